@@ -1,0 +1,214 @@
+"""Benchmark: lego NeRF training rays/s (forward + backward, 64 coarse + 128 fine samples).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step is one full training step of the reference hot path on one GPU's batch:
+4096 random rays (GPU ray generation from a 100-view 800x800 synthetic lego-shaped scene)
+-> stratified sampling -> coarse MLP -> compositing -> importance sampling + merge -> fine
+MLP -> compositing -> MSE(c)+MSE(f) -> backward of everything -> gradient all-reduce
+(RCCL, N > 1) -> fused clip_grad_value_(40) + Adam.  Weak scaling: 4096 rays per GPU.
+Weights: the reference's seed-0 init (torch.manual_seed(0); Network()).  Data is
+synthetic (no dataset offline).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("NERF_AMD_NO_ARGV", "1")
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "nerf-replication_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "train rays/sec (fwd+bwd, 64+128 samples) + 800x800 render s/frame, 1/2/4/8 GPU"
+# algorithmic FLOP per MLP sample: 593,408 MAC forward; backward dX 557,696 MAC
+# (no input grad for PE(xyz) at layers 0/5 and PE(dir) at the view layer), dW 593,408 MAC
+FLOP_PER_SAMPLE = {"mlp_fwd_train": 2 * 593408, "mlp_fwd": 2 * 593408, "mlp_bwd_dx": 2 * 557696,
+                   "mlp_bwd_dw": 2 * 593408}
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rays", type=int, default=4096, help="rays per GPU per step")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--images", type=int, default=100)
+    ap.add_argument("--res", type=int, default=800)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-render", action="store_true")
+    ap.add_argument("--cpu-rays", type=int, default=1024)
+    return ap.parse_args()
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
+    return world, rank, torch.device("cuda", local)
+
+
+def build(args, device):
+    from src.config import cfg
+    cfg.task_arg.mlp_dtype = args.dtype
+    cfg.task_arg.train_rays = args.rays
+    cfg.task_arg.perturb = 1
+    from src.datasets.nerf.blender import Dataset
+    from src.models import make_network
+    from src.train.optimizer import make_optimizer
+    from src.train.trainers.make_trainer import make_trainer
+    from src.utils.camera import focal_for, pose_spherical
+
+    torch.manual_seed(0)
+    net = make_network(cfg)  # reference init order + seed
+    trainer = make_trainer(cfg, net)
+    opt = make_optimizer(cfg, net)
+    thetas = torch.linspace(-180.0, 180.0, args.images + 1)[:-1]
+    poses = torch.stack([pose_spherical(float(t), -30.0, 4.0) for t in thetas]).to(device)
+    g = torch.Generator(device=device).manual_seed(1234)
+    images = torch.rand(args.images, args.res, args.res, 3, device=device, generator=g)
+    ds = Dataset.from_arrays(images, poses, focal_for(args.res))
+    return cfg, net, trainer, opt, ds
+
+
+def train_step(cfg, trainer, opt, ds, device):
+    rays, rgbs = ds.sample_batch()
+    batch = {"rays": rays[None], "rgbs": rgbs[None], "near": torch.tensor([2.0], device=device),
+             "far": torch.tensor([6.0], device=device)}
+    return trainer.train_step(batch, opt)
+
+
+def render_frame_time(cfg, net, ds, device, reps=2):
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    r = Renderer(net)
+    perturb = cfg.task_arg.perturb
+    cfg.task_arg.perturb = 0
+    rays, _ = ds.image_rays(0)
+    batch = {"rays": rays, "near": torch.tensor([2.0], device=device), "far": torch.tensor([6.0], device=device)}
+    net.eval()
+    times = []
+    with torch.no_grad():
+        r.render(batch)
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r.render(batch)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+    net.train()
+    cfg.task_arg.perturb = perturb
+    return min(times)
+
+
+def cpu_baseline(n_rays):
+    """The oracle (tests-only CPU restatement of the reference, torch CPU) on a bounded
+    sample: one n_rays forward+backward render (perturb 0), config 1 of BASELINE.json."""
+    from oracle import nerf_oracle as O
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    state = {k: v.clone().requires_grad_(True) for k, v in O.seeded_network_state(0).items()}
+    C, Fn = O.split_params(state, "model"), O.split_params(state, "model_fine")
+    pose = O.pose_spherical(30.0, -30.0, 4.0)
+    o, d = O.get_rays(800, 800, O.focal_from_angle(800, 0.6911112070083618), pose)
+    idx = torch.randint(0, 800 * 800, (n_rays,), generator=torch.Generator().manual_seed(0))
+    rays = torch.cat([o.reshape(-1, 3)[idx], d.reshape(-1, 3)[idx]], 1)
+    gt = torch.rand(n_rays, 3, generator=torch.Generator().manual_seed(1))
+
+    def once():
+        for v in state.values():
+            v.grad = None
+        ret = O.render(C, Fn, rays, torch.tensor([2.0]), torch.tensor([6.0]))
+        O.loss_fn(ret, gt)[0].backward()
+
+    once()
+    t0 = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        once()
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(n_rays / dt, 2), "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n_rays}-ray forward+backward render (64+128 samples, perturb 0, seed-0 weights), "
+                      f"mean of {reps} after 1 warm-up, torch {torch.__version__} CPU"}
+
+
+def main():
+    args = parse()
+    world, rank, device = setup_dist()
+    from nerf_amd import ops
+    cfg, net, trainer, opt, ds = build(args, device)
+
+    for _ in range(args.warmup):
+        train_step(cfg, trainer, opt, ds, device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.KERNEL_TIMES.reset()
+    ops.KERNEL_TIMES.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        train_step(cfg, trainer, opt, ds, device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ops.KERNEL_TIMES.enabled = False
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    ktimes = ops.KERNEL_TIMES.summary()
+
+    rays_total = world * args.rays * args.steps
+    value = rays_total / elapsed
+    # dominant kernel: largest total device time among the MLP kernels
+    name, (n_launch, ms, units) = max(ktimes.items(), key=lambda kv: kv[1][1])
+    avg_ms = ms / n_launch
+    flop_per_launch = FLOP_PER_SAMPLE.get(name, 0) * units / n_launch
+    achieved = flop_per_launch / (avg_ms * 1e-3) / 1e12
+    kt = {k: {"launches": n, "avg_ms": round(m / n, 4), "samples_per_launch": u // n,
+              "tflops": round(FLOP_PER_SAMPLE.get(k, 0) * (u / n) / (m / n * 1e-3) / 1e12, 2)}
+          for k, (n, m, u) in ktimes.items()}
+
+    render_s = None
+    if rank == 0 and not args.no_render and world == 1:
+        render_s = render_frame_time(cfg, net, ds, device)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_rays)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (100 spherical 800x800 views, random rgb; seed-0 reference init)",
+            "config": {"workload": "lego NeRF train step: coarse 64 + fine 128 samples/ray, 4096 rays/GPU, "
+                                   "MSE(c)+MSE(f), clip 40 + Adam",
+                       "rays_per_gpu": args.rays, "global_batch_rays": args.rays * world,
+                       "samples_per_ray": 64 + 192, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2),
+                         "peak": PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_TFLOPS[args.dtype], 4), "traffic": None,
+                         "flop_per_launch": flop_per_launch, "avg_launch_ms": round(avg_ms, 4)},
+            "kernels": kt,
+            "render_s_per_frame": None if render_s is None else round(render_s, 4),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

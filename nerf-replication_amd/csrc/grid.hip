@@ -1,0 +1,403 @@
+// Occupancy grid on gfx950: cell lookup, baking (grid update) and the grid-accelerated
+// ray march with early ray termination.
+//
+// Reference semantics (echo636/nerf-replication):
+//   world_to_grid_indices   src/models/nerf/renderer/volume_renderer.py:261-265
+//   render_accelerated      volume_renderer.py:268-357
+//   grid bake               occupancy_grid.py:15-80
+//
+// The reference marches all alive rays one t-step at a time (800 Python iterations, a
+// host sync each).  Here each round lets every alive ray collect its next K occupied
+// steps (gather), the fine MLP runs once on all collected points, and a per-ray
+// compositor consumes them in t order, stopping exactly where the reference would
+// (T < threshold after a queried step).  Points past a ray's termination are evaluated
+// but never composited, so outputs are those of the step-by-step march.
+#include "common.h"
+
+namespace nerf {
+
+struct BBox { float mn[3], mx[3]; };
+
+__device__ __forceinline__ int grid_axis(float p, float mn, float mx, int res) {
+  const float c = fminf(fmaxf(p, mn), mx);                  // torch.clamp(p, min, max)
+  const float n = fdiv(fsub(c, mn), fsub(mx, mn));          // (p - min) / (max - min)
+  return (int)fmul(n, (float)(res - 1));                    // (n * (res - 1)).long()
+}
+
+struct GridIndexArgs {
+  const float* pts;
+  int64_t M;
+  BBox bb;
+  int res;
+  const uint8_t* grid;
+  int64_t* idx;
+  uint8_t* occ;
+};
+
+__global__ void grid_index_kernel(GridIndexArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.M) return;
+  int ix = grid_axis(a.pts[i * 3 + 0], a.bb.mn[0], a.bb.mx[0], a.res);
+  int iy = grid_axis(a.pts[i * 3 + 1], a.bb.mn[1], a.bb.mx[1], a.res);
+  int iz = grid_axis(a.pts[i * 3 + 2], a.bb.mn[2], a.bb.mx[2], a.res);
+  if (a.idx) {
+    a.idx[i * 3 + 0] = ix;
+    a.idx[i * 3 + 1] = iy;
+    a.idx[i * 3 + 2] = iz;
+  }
+  if (a.occ) a.occ[i] = a.grid[((int64_t)ix * a.res + iy) * a.res + iz];
+}
+
+// ------------------------------------------------------------------------------------
+// bake
+// ------------------------------------------------------------------------------------
+struct BakeArgs {
+  int res;
+  BBox bb;
+  int dedup;   // 1: (res+1)^3 lattice points; 0: res^3 x 8 corners
+  float* pts;
+};
+
+__device__ __forceinline__ float voxel_size(const BBox& bb, int k, int res) {
+  return fdiv(fsub(bb.mx[k], bb.mn[k]), (float)res);
+}
+
+__global__ void bake_points_kernel(BakeArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a.dedup) {
+    const int64_t n = (int64_t)(a.res + 1);
+    if (i >= n * n * n) return;
+    const int L[3] = {(int)(i / (n * n)), (int)((i / n) % n), (int)(i % n)};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      a.pts[i * 3 + k] = fadd(a.bb.mn[k], fmul((float)L[k], voxel_size(a.bb, k, a.res)));
+  } else {
+    const int64_t n = (int64_t)a.res;
+    if (i >= n * n * n * 8) return;
+    const int64_t v = i >> 3;
+    const int c = (int)(i & 7);  // meshgrid 'ij' over the 2x2x2 corner offsets
+    const int idx[3] = {(int)(v / (n * n)), (int)((v / n) % n), (int)(v % n)};
+    const int off[3] = {(c >> 2) & 1, (c >> 1) & 1, c & 1};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float vs = voxel_size(a.bb, k, a.res);
+      const float base = fadd(a.bb.mn[k], fmul((float)idx[k], vs));
+      a.pts[i * 3 + k] = fadd(base, off[k] ? vs : 0.f);
+    }
+  }
+}
+
+struct BakeReduceArgs {
+  const float* raw;  // [P,4]
+  int res, dedup;
+  float threshold;
+  uint8_t* grid;     // [res^3]
+};
+
+__global__ void bake_reduce_kernel(BakeReduceArgs a) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = a.res;
+  if (v >= n * n * n) return;
+  const int x = (int)(v / (n * n)), y = (int)((v / n) % n), z = (int)(v % n);
+  bool occ = false;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    int64_t p;
+    if (a.dedup) {
+      const int64_t m = n + 1;
+      p = ((int64_t)(x + ((c >> 2) & 1)) * m + (y + ((c >> 1) & 1))) * m + (z + (c & 1));
+    } else {
+      p = v * 8 + c;
+    }
+    const float s = a.raw[p * 4 + 3];
+    const float sigma = s > 0.f ? s : 0.f;  // relu(raw[..., 3])
+    occ |= sigma > a.threshold;
+  }
+  a.grid[v] = occ ? 1 : 0;
+}
+
+// ------------------------------------------------------------------------------------
+// march
+// ------------------------------------------------------------------------------------
+struct MarchState {
+  float* T;
+  float* rgb;
+  float* depth;
+  float* acc;
+  int32_t* next_step;
+  uint8_t* alive;     // 1 = still marching
+  uint8_t* exhausted; // 1 = gather reached the end of the t table
+};
+
+struct MarchGatherArgs {
+  const float* rays;  // [N,6]
+  int64_t N;
+  const float* t_table;
+  int n_steps;
+  const uint8_t* grid;
+  int res;
+  BBox bb;
+  int K;
+  MarchState st;
+  int32_t* counters;   // [0] points written, [1] rays alive after gather
+  int32_t* out_ray;    // [cap]
+  int32_t* out_step;   // [cap]
+  float* out_pts;      // [cap,3]
+  int32_t* ray_off;    // [N]
+  int32_t* ray_cnt;    // [N]
+  int64_t cap;
+};
+
+__device__ __forceinline__ bool march_occupied(const MarchGatherArgs& a, const float* ray, float t, float* p) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = fadd(ray[k], fmul(t, ray[3 + k]));  // o + t * d
+  const int ix = grid_axis(p[0], a.bb.mn[0], a.bb.mx[0], a.res);
+  const int iy = grid_axis(p[1], a.bb.mn[1], a.bb.mx[1], a.res);
+  const int iz = grid_axis(p[2], a.bb.mn[2], a.bb.mx[2], a.res);
+  return a.grid[((int64_t)ix * a.res + iy) * a.res + iz] != 0;
+}
+
+__global__ void march_gather_kernel(MarchGatherArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = r < a.N;
+  const bool live = in && a.st.alive[r];
+  int cnt = 0, s = live ? a.st.next_step[r] : 0;
+  const float* ray = a.rays + (in ? r : 0) * 6;
+  float p[3];
+  if (live) {
+    for (; s < a.n_steps && cnt < a.K; ++s)
+      if (march_occupied(a, ray, a.t_table[s], p)) ++cnt;
+  }
+  // wave-aggregated reservation
+  const int l = lane_id();
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int t = __shfl_up(incl, o, 64);
+    if (l >= o) incl += t;
+  }
+  const int wtotal = __shfl(incl, 63, 64);
+  int base = 0;
+  if (l == 63 && wtotal > 0) base = atomicAdd(&a.counters[0], wtotal);
+  base = __shfl(base, 63, 64);
+  const unsigned long long live_mask = __ballot(live);
+  if (l == 0 && live_mask) atomicAdd(&a.counters[1], __popcll(live_mask));
+  if (!in) return;
+  if (!live) {
+    a.ray_cnt[r] = 0;
+    return;
+  }
+  int pos = base + incl - cnt;
+  const bool overflow = (int64_t)pos + cnt > a.cap;
+  a.ray_off[r] = pos;
+  a.ray_cnt[r] = overflow ? 0 : cnt;
+  a.st.exhausted[r] = (s >= a.n_steps) ? 1 : 0;
+  if (overflow) return;  // caller sizes cap = N*K, never taken
+  a.st.next_step[r] = s;
+}
+
+// Two-pass variant that keeps the start step: the gather kernel above records counts;
+// this kernel writes the points.
+struct MarchEmitArgs {
+  MarchGatherArgs g;
+  const int32_t* start_step;  // [N] step before the gather
+};
+
+__global__ void march_emit_kernel(MarchEmitArgs e) {
+  const MarchGatherArgs& a = e.g;
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.N) return;
+  const int cnt = a.ray_cnt[r];
+  if (cnt == 0) return;
+  const float* ray = a.rays + r * 6;
+  int pos = a.ray_off[r];
+  int k = 0;
+  float p[3];
+  for (int s = e.start_step[r]; k < cnt; ++s) {
+    if (march_occupied(a, ray, a.t_table[s], p)) {
+      a.out_ray[pos + k] = (int32_t)r;
+      a.out_step[pos + k] = s;
+      a.out_pts[(int64_t)(pos + k) * 3 + 0] = p[0];
+      a.out_pts[(int64_t)(pos + k) * 3 + 1] = p[1];
+      a.out_pts[(int64_t)(pos + k) * 3 + 2] = p[2];
+      ++k;
+    }
+  }
+}
+
+struct MarchCompArgs {
+  const float* raw;  // [cap,4]
+  const float* rays;
+  int64_t N;
+  const float* t_table;
+  const int32_t* ray_off;
+  const int32_t* ray_cnt;
+  const int32_t* out_step;
+  MarchState st;
+  float step_size, t_thresh;
+};
+
+__global__ void march_composite_kernel(MarchCompArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.N || !a.st.alive[r]) return;
+  const int cnt = a.ray_cnt[r], off = a.ray_off[r];
+  const float* ray = a.rays + r * 6;
+  const float dx = ray[3], dy = ray[4], dz = ray[5];
+  const float dist = fmul(a.step_size, sqrtf(fadd(fadd(fmul(dx, dx), fmul(dy, dy)), fmul(dz, dz))));
+  float T = a.st.T[r];
+  float cr = a.st.rgb[r * 3 + 0], cg = a.st.rgb[r * 3 + 1], cb = a.st.rgb[r * 3 + 2];
+  float dep = a.st.depth[r], acc = a.st.acc[r];
+  bool alive = true;
+  for (int k = 0; k < cnt; ++k) {
+    const float4 rw = *(const float4*)(a.raw + (int64_t)(off + k) * 4);
+    const float t = a.t_table[a.out_step[off + k]];
+    const float sr = 1.f / (1.f + expf(-rw.x)), sg = 1.f / (1.f + expf(-rw.y)), sb = 1.f / (1.f + expf(-rw.z));
+    const float sigma = rw.w > 0.f ? rw.w : 0.f;
+    const float alpha = fsub(1.f, expf(-fmul(sigma, dist)));
+    const float ta = fmul(T, alpha);
+    cr = fadd(cr, fmul(ta, sr));
+    cg = fadd(cg, fmul(ta, sg));
+    cb = fadd(cb, fmul(ta, sb));
+    acc = fadd(acc, ta);
+    dep = fadd(dep, fmul(ta, t));
+    T = fmul(T, fsub(1.f, alpha));
+    if (T < a.t_thresh) {
+      alive = false;
+      break;
+    }
+  }
+  a.st.T[r] = T;
+  a.st.rgb[r * 3 + 0] = cr;
+  a.st.rgb[r * 3 + 1] = cg;
+  a.st.rgb[r * 3 + 2] = cb;
+  a.st.depth[r] = dep;
+  a.st.acc[r] = acc;
+  if (!alive || a.st.exhausted[r]) a.st.alive[r] = 0;
+}
+
+struct MarchInitArgs { MarchState st; int64_t N; };
+__global__ void march_init_kernel(MarchInitArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.N) return;
+  a.st.T[r] = 1.f;
+  a.st.rgb[r * 3 + 0] = a.st.rgb[r * 3 + 1] = a.st.rgb[r * 3 + 2] = 0.f;
+  a.st.depth[r] = 0.f;
+  a.st.acc[r] = 0.f;
+  a.st.next_step[r] = 0;
+  a.st.alive[r] = 1;
+  a.st.exhausted[r] = 0;
+}
+
+struct MarchFinishArgs { MarchState st; int64_t N; int white; };
+__global__ void march_finish_kernel(MarchFinishArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.N || !a.white) return;
+  const float bg = fsub(1.f, a.st.acc[r]);  // rgb += (1 - acc) * 1
+#pragma unroll
+  for (int k = 0; k < 3; ++k) a.st.rgb[r * 3 + k] = fadd(a.st.rgb[r * 3 + k], bg);
+}
+
+}  // namespace nerf
+
+// ======================================================================================
+// C-ABI
+// ======================================================================================
+using namespace nerf;
+
+static BBox make_bbox(const float* b) {
+  BBox bb;
+  for (int k = 0; k < 3; ++k) {
+    bb.mn[k] = b[k];
+    bb.mx[k] = b[3 + k];
+  }
+  return bb;
+}
+
+static inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+extern "C" {
+
+int nerf_grid_index(const float* pts, int64_t M, const float* bbox_host, int res, const uint8_t* grid,
+                    int64_t* idx_out, uint8_t* occ_out, hipStream_t stream) {
+  NERF_REQUIRE(M >= 0 && res > 1 && bbox_host, "nerf_grid_index: bad arguments");
+  if (M == 0) return 0;
+  NERF_REQUIRE(pts && (idx_out || occ_out), "nerf_grid_index: null pointer");
+  NERF_REQUIRE(!occ_out || grid, "nerf_grid_index: occupancy needs the grid");
+  GridIndexArgs a{pts, M, make_bbox(bbox_host), res, grid, idx_out, occ_out};
+  hipLaunchKernelGGL(grid_index_kernel, grid1(M), dim3(256), 0, stream, a);
+  return check_launch("nerf_grid_index");
+}
+
+int64_t nerf_bake_num_points(int res, int dedup) {
+  const int64_t n = res;
+  return dedup ? (n + 1) * (n + 1) * (n + 1) : n * n * n * 8;
+}
+
+int nerf_bake_points(int res, const float* bbox_host, int dedup, float* pts, hipStream_t stream) {
+  NERF_REQUIRE(res > 0 && bbox_host && pts, "nerf_bake_points: bad arguments");
+  BakeArgs a{res, make_bbox(bbox_host), dedup, pts};
+  hipLaunchKernelGGL(bake_points_kernel, grid1(nerf_bake_num_points(res, dedup)), dim3(256), 0, stream, a);
+  return check_launch("nerf_bake_points");
+}
+
+int nerf_bake_reduce(const float* raw, int res, int dedup, float threshold, uint8_t* grid, hipStream_t stream) {
+  NERF_REQUIRE(res > 0 && raw && grid, "nerf_bake_reduce: bad arguments");
+  BakeReduceArgs a{raw, res, dedup, threshold, grid};
+  hipLaunchKernelGGL(bake_reduce_kernel, grid1((int64_t)res * res * res), dim3(256), 0, stream, a);
+  return check_launch("nerf_bake_reduce");
+}
+
+// state: T, rgb[3], depth, acc (f32) ; next_step (i32) ; alive, exhausted (u8)
+int nerf_march_init(float* T, float* rgb, float* depth, float* acc, int32_t* next_step, uint8_t* alive,
+                    uint8_t* exhausted, int64_t N, hipStream_t stream) {
+  if (N == 0) return 0;
+  NERF_REQUIRE(T && rgb && depth && acc && next_step && alive && exhausted, "nerf_march_init: null pointer");
+  MarchInitArgs a{{T, rgb, depth, acc, next_step, alive, exhausted}, N};
+  hipLaunchKernelGGL(march_init_kernel, grid1(N), dim3(256), 0, stream, a);
+  return check_launch("nerf_march_init");
+}
+
+// counters[0] = points emitted, counters[1] = rays alive entering this round (zero them first).
+// start_step_scratch: [N] int32 workspace.
+int nerf_march_gather(const float* rays, int64_t N, const float* t_table, int n_steps, const uint8_t* grid, int res,
+                      const float* bbox_host, int K, float* T, float* rgb, float* depth, float* acc,
+                      int32_t* next_step, uint8_t* alive, uint8_t* exhausted, int32_t* counters,
+                      int32_t* start_step_scratch, int32_t* out_ray, int32_t* out_step, float* out_pts,
+                      int32_t* ray_off, int32_t* ray_cnt, int64_t cap, hipStream_t stream) {
+  NERF_REQUIRE(N >= 0 && n_steps >= 0 && K > 0 && res > 1 && bbox_host, "nerf_march_gather: bad arguments");
+  NERF_REQUIRE(cap >= N * (int64_t)K, "nerf_march_gather: cap must be >= N*K");
+  if (N == 0) return 0;
+  MarchGatherArgs a{rays, N, t_table, n_steps, grid, res, make_bbox(bbox_host), K,
+                    {T, rgb, depth, acc, next_step, alive, exhausted},
+                    counters, out_ray, out_step, out_pts, ray_off, ray_cnt, cap};
+  if (hipMemcpyAsync(start_step_scratch, next_step, N * sizeof(int32_t), hipMemcpyDeviceToDevice, stream) !=
+      hipSuccess) {
+    set_error("nerf_march_gather: hipMemcpyAsync failed");
+    return -5;
+  }
+  hipLaunchKernelGGL(march_gather_kernel, grid1(N), dim3(256), 0, stream, a);
+  if (int e = check_launch("nerf_march_gather")) return e;
+  MarchEmitArgs em{a, start_step_scratch};
+  hipLaunchKernelGGL(march_emit_kernel, grid1(N), dim3(256), 0, stream, em);
+  return check_launch("nerf_march_emit");
+}
+
+int nerf_march_composite(const float* raw, const float* rays, int64_t N, const float* t_table, const int32_t* ray_off,
+                         const int32_t* ray_cnt, const int32_t* out_step, float* T, float* rgb, float* depth,
+                         float* acc, int32_t* next_step, uint8_t* alive, uint8_t* exhausted, float step_size,
+                         float t_thresh, hipStream_t stream) {
+  if (N == 0) return 0;
+  MarchCompArgs a{raw, rays, N, t_table, ray_off, ray_cnt, out_step,
+                  {T, rgb, depth, acc, next_step, alive, exhausted}, step_size, t_thresh};
+  hipLaunchKernelGGL(march_composite_kernel, grid1(N), dim3(256), 0, stream, a);
+  return check_launch("nerf_march_composite");
+}
+
+int nerf_march_finish(float* rgb, const float* acc, int64_t N, int white, hipStream_t stream) {
+  if (N == 0) return 0;
+  MarchFinishArgs a{{nullptr, rgb, nullptr, const_cast<float*>(acc), nullptr, nullptr, nullptr}, N, white};
+  hipLaunchKernelGGL(march_finish_kernel, grid1(N), dim3(256), 0, stream, a);
+  return check_launch("nerf_march_finish");
+}
+
+}  // extern "C"

@@ -1,0 +1,182 @@
+// Compile-time layout of the lego NeRF MLP on MFMA tiles.
+//
+// Reference: src/models/nerf/network.py:9-74 (NeRF: D=8, W=256, skips=[4], use_viewdirs)
+// with the frequency encoders of src/models/encoding/freq.py (xyz L=10 -> 63, dir L=4 -> 27).
+//
+// Every matrix product is computed "feature-major": an accumulator tile is 32 features x
+// 32 samples (v_mfma_f32_32x32x{16_bf16,2_f32}); lane l holds sample (l & 31) and, in
+// its 16 accumulator registers rho, feature acc_row(rho, l >> 5).  A layer's input is a
+// list of such 32-feature tiles (the previous layer's accumulators, or the positional
+// encoding laid out the same way), so one layer's output feeds the next MFMA's B
+// operand straight from registers.  Weights (A operand) are re-packed once per optimizer
+// step into 1 KiB lane-linear "chunks" (64 lanes x 16 B) in exactly that k order.
+#pragma once
+#include <stdint.h>
+
+namespace nerf {
+namespace mlp {
+
+__host__ __device__ constexpr int acc_row(int rho, int h) { return (rho & 3) + 8 * (rho >> 2) + 4 * h; }
+
+// forward layers (in execution order)
+enum Layer { L0 = 0, L1, L2, L3, L4, L5, L6, L7, LFA, LV, LRGB, NLAYER };
+
+// parameter slots, state_dict order of one NeRF (network.py:22-44)
+enum Param {
+  P_W0 = 0,  // pts_linears.i.weight = 2i, .bias = 2i+1 (i = 0..7)
+  P_VW = 16, P_VB = 17,   // views_linears.0
+  P_FW = 18, P_FB = 19,   // feature_linear
+  P_AW = 20, P_AB = 21,   // alpha_linear
+  P_RW = 22, P_RB = 23,   // rgb_linear
+  NPARAM = 24
+};
+
+// in_features of each weight (row stride of nn.Linear's [out, in] weight)
+__host__ __device__ constexpr int weight_K(int p) {
+  return p == 0 ? 63 : p == 10 ? 319 : p == P_VW ? 283 : p == P_RW ? 128 : 256;
+}
+__host__ __device__ constexpr int weight_N(int p) {
+  return p == P_VW ? 128 : p == P_AW ? 1 : p == P_RW ? 3 : 256;
+}
+// element offsets of every parameter in the flat state_dict-order gradient buffer
+__host__ __device__ constexpr int64_t param_numel(int i) {
+  return (i & 1) ? weight_N(i - 1) : (int64_t)weight_N(i) * weight_K(i);
+}
+__host__ __device__ constexpr int64_t param_offset(int i) {
+  int64_t o = 0;
+  for (int k = 0; k < i; ++k) o += param_numel(k);
+  return o;
+}
+constexpr int64_t NET_PARAMS = param_offset(NPARAM);  // 595,844
+static_assert(NET_PARAMS == 595844, "NeRF parameter count");
+
+// number of input tiles / output tiles per forward layer
+__host__ __device__ constexpr int fwd_in_tiles(int L) {
+  return L == L0 ? 2 : L == L5 ? 10 : L == LV ? 9 : L == LRGB ? 4 : 8;
+}
+__host__ __device__ constexpr int fwd_out_tiles(int L) {
+  return L == LFA ? 9 : L == LV ? 4 : L == LRGB ? 1 : 8;
+}
+// input tile t of layer L -> (first weight column, number of valid columns)
+__host__ __device__ constexpr int fwd_in_colbase(int L, int t) {
+  return L == L0 ? 32 * t
+       : L == L5 ? (t < 2 ? 32 * t : 63 + 32 * (t - 2))
+       : L == LV ? 32 * t
+       : 32 * t;
+}
+__host__ __device__ constexpr int fwd_in_valid(int L, int t) {
+  return (L == L0 || L == L5) && t == 1 ? 31 : (L == LV && t == 8) ? 27 : 32;
+}
+// output tile n of layer L -> weight param, first weight row, valid rows, bias param
+__host__ __device__ constexpr int fwd_out_weight(int L, int n) {
+  return L <= L7 ? 2 * L : L == LFA ? (n < 8 ? (int)P_FW : (int)P_AW) : L == LV ? (int)P_VW : (int)P_RW;
+}
+__host__ __device__ constexpr int fwd_out_row0(int L, int n) { return (L == LFA && n == 8) ? 0 : 32 * n; }
+__host__ __device__ constexpr int fwd_out_valid(int L, int n) {
+  return (L == LFA && n == 8) ? 1 : L == LRGB ? 3 : 32;
+}
+
+// forward units: one per (layer, output tile), in execution order
+constexpr int NUNIT_FWD = 8 * 8 + 9 + 4 + 1;  // 78
+__host__ __device__ constexpr int fwd_unit_first(int L) {
+  int u = 0;
+  for (int k = 0; k < L; ++k) u += fwd_out_tiles(k);
+  return u;
+}
+__host__ __device__ constexpr int fwd_unit_layer(int u) {
+  int L = 0;
+  while (L < NLAYER - 1 && u >= fwd_unit_first(L + 1)) ++L;
+  return L;
+}
+__host__ __device__ constexpr int fwd_unit_tiles(int u) { return fwd_in_tiles(fwd_unit_layer(u)); }
+__host__ __device__ constexpr int fwd_unit_tile_off(int u) {  // in input tiles
+  int o = 0;
+  for (int k = 0; k < u; ++k) o += fwd_unit_tiles(k);
+  return o;
+}
+constexpr int FWD_TILES = fwd_unit_tile_off(NUNIT_FWD);  // 592
+
+// backward (dX chain) units, W^T products, in execution order:
+//   bRGB (4 out tiles: hv), bV (8: feature), bFA (8: h7), b7, b6, b5 (-> h4), b4, b3, b2, b1 (-> h0)
+enum BStage { B_RGB = 0, B_V, B_FA, B_7, B_6, B_5, B_4, B_3, B_2, B_1, NBSTAGE };
+__host__ __device__ constexpr int bwd_fwd_layer(int s) {
+  return s == B_RGB ? LRGB : s == B_V ? LV : s == B_FA ? LFA : (L7 - (s - B_7));
+}
+__host__ __device__ constexpr int bwd_out_tiles(int s) { return s == B_RGB ? 4 : 8; }
+__host__ __device__ constexpr int bwd_in_tiles(int s) { return fwd_out_tiles(bwd_fwd_layer(s)); }
+// output tile j of stage s -> first column of the forward weight it reads
+__host__ __device__ constexpr int bwd_out_colbase(int s, int j) {
+  return bwd_fwd_layer(s) == L5 ? 63 + 32 * j : 32 * j;
+}
+constexpr int NUNIT_BWD = 4 + 8 * 9;  // 76
+__host__ __device__ constexpr int bwd_unit_first(int s) {
+  int u = 0;
+  for (int k = 0; k < s; ++k) u += bwd_out_tiles(k);
+  return u;
+}
+__host__ __device__ constexpr int bwd_unit_stage(int u) {
+  int s = 0;
+  while (s < NBSTAGE - 1 && u >= bwd_unit_first(s + 1)) ++s;
+  return s;
+}
+__host__ __device__ constexpr int bwd_unit_tiles(int u) { return bwd_in_tiles(bwd_unit_stage(u)); }
+__host__ __device__ constexpr int bwd_unit_tile_off(int u) {
+  int o = 0;
+  for (int k = 0; k < u; ++k) o += bwd_unit_tiles(k);
+  return o;
+}
+constexpr int BWD_TILES = bwd_unit_tile_off(NUNIT_BWD);
+
+// feature-major activation store (rows x M_pad), written by the training forward
+enum ActRow {
+  A_X = 0,       // PE(xyz): 63 rows (+1 zero pad)
+  A_D = 64,      // PE(dir): 27 rows (+5 zero pad)
+  A_H = 96,      // h0..h7 post-ReLU: 8 x 256
+  A_F = 96 + 2048,  // feature (no activation): 256
+  A_V = A_F + 256,  // views hidden post-ReLU: 128
+  A_ROWS = A_V + 128  // 2528
+};
+// feature-major output-gradient store, written by the dX chain
+enum DzRow {
+  Z_H = 0,             // dZ0..dZ7 (pre-ReLU grads of pts_linears): 8 x 256
+  Z_F = 2048,          // d feature: 256
+  Z_A = Z_F + 256,     // d alpha: row 0 of a 32-row block
+  Z_V = Z_A + 32,      // dZ views: 128
+  Z_RGB = Z_V + 128,   // d rgb: rows 0..2 of a 32-row block
+  Z_ROWS = Z_RGB + 32  // 2496
+};
+// ReLU masks: per 32-sample wave block, 68 tiles x 64 lanes x 16 bits
+constexpr int MASK_TILES = 68;  // h0..h7 (8x8), hv (4)
+
+// dW GEMM list (per net): C[n][k] = sum_m dz[n][m] act[k][m]
+//   g: (dz row base, n tiles, weight param, bias param, k tiles, act rows per k tile)
+constexpr int NGEMM = 12;
+__host__ __device__ constexpr int gemm_weight(int g) {
+  return g < 8 ? 2 * g : g == 8 ? (int)P_FW : g == 9 ? (int)P_AW : g == 10 ? (int)P_VW : (int)P_RW;
+}
+__host__ __device__ constexpr int gemm_dz_row(int g) {
+  return g < 8 ? Z_H + 256 * g : g == 8 ? Z_F : g == 9 ? Z_A : g == 10 ? Z_V : Z_RGB;
+}
+__host__ __device__ constexpr int gemm_n_tiles(int g) { return g < 9 ? 8 : g == 9 ? 1 : g == 10 ? 4 : 1; }
+__host__ __device__ constexpr int gemm_n_valid(int g) { return g == 9 ? 1 : g == 11 ? 3 : 256; }
+__host__ __device__ constexpr int gemm_k_tiles(int g) {
+  return g == 0 ? 2 : g == 5 ? 10 : g == 10 ? 9 : g == 11 ? 4 : 8;
+}
+// k tile t of gemm g -> (act row base, first weight column, valid columns)
+__host__ __device__ constexpr int gemm_act_row(int g, int t) {
+  return g == 0 ? A_X + 32 * t
+       : g == 5 ? (t < 2 ? A_X + 32 * t : A_H + 256 * 4 + 32 * (t - 2))
+       : g <= 7 ? A_H + 256 * (g - 1) + 32 * t
+       : g <= 9 ? A_H + 256 * 7 + 32 * t
+       : g == 10 ? (t < 8 ? A_F + 32 * t : A_D)
+       : A_V + 32 * t;
+}
+__host__ __device__ constexpr int gemm_col0(int g, int t) {
+  return g == 0 ? 32 * t : g == 5 ? (t < 2 ? 32 * t : 63 + 32 * (t - 2)) : 32 * t;
+}
+__host__ __device__ constexpr int gemm_col_valid(int g, int t) {
+  return (g == 0 || g == 5) && t == 1 ? 31 : (g == 10 && t == 8) ? 27 : 32;
+}
+
+}  // namespace mlp
+}  // namespace nerf

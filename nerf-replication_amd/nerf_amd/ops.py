@@ -1,0 +1,515 @@
+"""Torch-facing wrappers of the gfx950 kernels (device memory and streams come from torch;
+the arithmetic is in libnerf_amd.so).  Every function raises on CPU tensors.
+
+Reference interfaces mirrored (echo636/nerf-replication):
+  raygen               src/datasets/nerf/blender.py:13-32, 124-131
+  sample_stratified    src/models/nerf/renderer/volume_renderer.py:165-187
+  sample_pdf           volume_renderer.py:82-134 (+ merge :205-221)
+  composite            volume_renderer.py:20-80 (autograd Function)
+  mlp                  src/models/nerf/network.py:171-192 (autograd Function)
+  grid_index           volume_renderer.py:261-265
+  march                volume_renderer.py:268-357
+  bake                 occupancy_grid.py:15-80
+  adam_step            src/train/trainers/trainer.py:61-62
+"""
+from __future__ import annotations
+
+import ctypes as _ctypes
+import functools
+from typing import List, Optional, Sequence
+
+import torch
+
+from ._lib import check, lib, ptr, stream_of
+
+F32, BF16 = 0, 1
+DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16}
+
+SCENE_BBOX = ((-1.5, -1.5, -1.5), (1.5, 1.5, 1.5))
+
+
+def dtype_code(d) -> int:
+    if isinstance(d, int):
+        return d
+    if d not in DTYPES:
+        raise ValueError(f"unsupported MLP dtype {d!r} (fp32 or bf16)")
+    return DTYPES[d]
+
+
+def _f32c(t: torch.Tensor, name: str) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+    return t.contiguous()
+
+
+@functools.lru_cache(maxsize=None)
+def _cpu_table(kind: str, a: float, b: float, n_or_step) -> torch.Tensor:
+    """Host CPU tables (torch.linspace / torch.arange evaluated on the CPU, as the reference)."""
+    if kind == "linspace":
+        return torch.linspace(a, b, steps=int(n_or_step))
+    return torch.arange(a, b, n_or_step)
+
+
+_dev_tables = {}
+
+
+def device_table(kind: str, a: float, b: float, n_or_step, device) -> torch.Tensor:
+    key = (kind, a, b, n_or_step, str(device))
+    t = _dev_tables.get(key)
+    if t is None:
+        t = _cpu_table(kind, a, b, n_or_step).to(device)
+        _dev_tables[key] = t
+    return t
+
+
+def _scalar_dev(x, device) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        return x.reshape(-1)[:1].to(device=device, dtype=torch.float32).contiguous()
+    return torch.tensor([float(x)], dtype=torch.float32, device=device)
+
+
+# --------------------------------------------------------------------------------------
+# optional per-kernel timing with HIP events on the launching stream (bench.py roofline)
+# --------------------------------------------------------------------------------------
+class _KernelTimes:
+    def __init__(self):
+        self.enabled = False
+        self.pending = []  # (name, units, start_event, end_event)
+
+    def reset(self):
+        self.pending = []
+
+    def summary(self):
+        """{name: (launches, total_ms, total_units)} -- synchronises on the recorded events."""
+        out = {}
+        for name, units, a, b in self.pending:
+            n, ms, u = out.get(name, (0, 0.0, 0))
+            out[name] = (n + 1, ms + a.elapsed_time(b), u + units)
+        return out
+
+
+KERNEL_TIMES = _KernelTimes()
+
+
+class kernel_timer:
+    def __init__(self, name, units):
+        self.name, self.units = name, units
+
+    def __enter__(self):
+        if KERNEL_TIMES.enabled:
+            self.a = torch.cuda.Event(enable_timing=True)
+            self.b = torch.cuda.Event(enable_timing=True)
+            self.a.record(torch.cuda.current_stream())
+        return self
+
+    def __exit__(self, *exc):
+        if KERNEL_TIMES.enabled:
+            self.b.record(torch.cuda.current_stream())
+            KERNEL_TIMES.pending.append((self.name, self.units, self.a, self.b))
+        return False
+
+
+# --------------------------------------------------------------------------------------
+# rays
+# --------------------------------------------------------------------------------------
+def raygen(c2w: torch.Tensor, H: int, W: int, focal: float, pix: Optional[torch.Tensor] = None, n_rays: int = 0,
+           seed: int = 0, offset: int = 0, images: Optional[torch.Tensor] = None, want_pix: bool = False):
+    """Pinhole rays for flat pixel ids (img*H*W + j*W + i) -> rays [R,6] (+ rgb [R,3])."""
+    c2w = _f32c(c2w.reshape(-1, 4, 4) if c2w.shape[-2:] == (4, 4) else c2w, "c2w")
+    if c2w.shape[-2:] != (4, 4):
+        raise ValueError("c2w must be [..., 4, 4]")
+    dev = c2w.device
+    R = int(pix.numel()) if pix is not None else int(n_rays)
+    if pix is not None:
+        pix = pix.to(device=dev, dtype=torch.int64).contiguous()
+    rays = torch.empty(R, 6, device=dev, dtype=torch.float32)
+    rgb = torch.empty(R, 3, device=dev, dtype=torch.float32) if images is not None else None
+    pout = torch.empty(R, device=dev, dtype=torch.int64) if want_pix else None
+    if images is not None:
+        images = _f32c(images, "images")
+    check(lib().nerf_raygen(ptr(c2w), c2w.shape[0], H, W, float(focal), ptr(pix), R, seed, offset, ptr(images),
+                            ptr(rays), ptr(rgb), ptr(pout), stream_of(c2w)), "nerf_raygen")
+    return rays, rgb, pout
+
+
+def sample_stratified(rays: torch.Tensor, near, far, n_samples: int, perturb: bool,
+                      t_rand: Optional[torch.Tensor] = None, seed: int = 0, offset: int = 0,
+                      want_pts: bool = True):
+    """-> z [R,S], pts [R,S,3] (or None), viewdirs [R,3]."""
+    rays = _f32c(rays.reshape(-1, 6), "rays")
+    dev, R = rays.device, rays.shape[0]
+    t_lin = device_table("linspace", 0.0, 1.0, n_samples, dev)
+    z = torch.empty(R, n_samples, device=dev, dtype=torch.float32)
+    pts = torch.empty(R, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
+    vd = torch.empty(R, 3, device=dev, dtype=torch.float32)
+    if t_rand is not None:
+        t_rand = _f32c(t_rand, "t_rand")
+    near_t, far_t = _scalar_dev(near, dev), _scalar_dev(far, dev)  # keep alive across the launch
+    check(lib().nerf_sample_stratified(ptr(rays), R, n_samples, ptr(t_lin), ptr(near_t), ptr(far_t),
+                                       int(bool(perturb)), ptr(t_rand), seed, offset, ptr(z), ptr(pts), ptr(vd),
+                                       stream_of(rays)), "nerf_sample_stratified")
+    return z, pts, vd
+
+
+def searchsorted(cdf: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
+    """torch.searchsorted(cdf, u, right=True) for rows of <= 64 sorted entries (int32)."""
+    cdf, u = _f32c(cdf, "cdf"), _f32c(u, "u")
+    R, nb = cdf.shape
+    out = torch.empty(u.shape, device=cdf.device, dtype=torch.int32)
+    check(lib().nerf_searchsorted(ptr(cdf), ptr(u), R, nb, u.shape[1], ptr(out), stream_of(cdf)), "nerf_searchsorted")
+    return out
+
+
+def sample_pdf(z: torch.Tensor, weights: torch.Tensor, n_importance: int, det: bool,
+               u: Optional[torch.Tensor] = None, seed: int = 0, offset: int = 0,
+               rays: Optional[torch.Tensor] = None, debug: bool = False):
+    """Importance sampling on the coarse weights + merge with z.
+
+    Returns dict(z_fine [R,Sc+Ni] sorted, pts_fine [R,Sc+Ni,3] if rays given, and with
+    ``debug`` samples [R,Ni], cdf [R,Sc-1], inds [R,Ni] int32).
+    """
+    z, weights = _f32c(z, "z"), _f32c(weights.detach(), "weights")
+    R, Sc = z.shape
+    dev = z.device
+    S = Sc + n_importance
+    out = {"z_fine": torch.empty(R, S, device=dev, dtype=torch.float32)}
+    if rays is not None:
+        rays = _f32c(rays.reshape(-1, 6), "rays")
+        out["pts_fine"] = torch.empty(R, S, 3, device=dev, dtype=torch.float32)
+    if debug:
+        out["samples"] = torch.empty(R, n_importance, device=dev, dtype=torch.float32)
+        out["cdf"] = torch.empty(R, Sc - 1, device=dev, dtype=torch.float32)
+        out["inds"] = torch.empty(R, n_importance, device=dev, dtype=torch.int32)
+    u_lin = device_table("linspace", 0.0, 1.0, n_importance, dev) if det else None
+    if u is not None:
+        u = _f32c(u, "u")
+    check(lib().nerf_sample_pdf(ptr(z), ptr(weights), R, Sc, n_importance, int(bool(det)), ptr(u_lin), ptr(u), seed,
+                                offset, ptr(rays), ptr(out["z_fine"]), ptr(out.get("pts_fine")),
+                                ptr(out.get("samples")), ptr(out.get("cdf")), ptr(out.get("inds")), stream_of(z)),
+          "nerf_sample_pdf")
+    return out
+
+
+def sample_pdf_bins(bins: torch.Tensor, weights: torch.Tensor, n_samples: int, det: bool,
+                    u: Optional[torch.Tensor] = None, seed: int = 0, offset: int = 0, debug: bool = False):
+    """Reference-signature sample_pdf: bins [R,nb], weights [R,nb-1] -> samples [R,N] (u order)."""
+    bins, weights = _f32c(bins, "bins"), _f32c(weights.detach(), "weights")
+    R, nb = bins.shape
+    dev = bins.device
+    samples = torch.empty(R, n_samples, device=dev, dtype=torch.float32)
+    cdf = torch.empty(R, nb, device=dev, dtype=torch.float32) if debug else None
+    inds = torch.empty(R, n_samples, device=dev, dtype=torch.int32) if debug else None
+    u_lin = device_table("linspace", 0.0, 1.0, n_samples, dev) if det else None
+    if u is not None:
+        u = _f32c(u, "u")
+    check(lib().nerf_sample_pdf_bins(ptr(bins), ptr(weights), R, nb, n_samples, int(bool(det)), ptr(u_lin), ptr(u),
+                                     seed, offset, ptr(samples), ptr(cdf), ptr(inds), stream_of(bins)),
+          "nerf_sample_pdf_bins")
+    return (samples, cdf, inds) if debug else samples
+
+
+# --------------------------------------------------------------------------------------
+# compositing (autograd)
+# --------------------------------------------------------------------------------------
+def _dirs_view(rays_d: torch.Tensor):
+    """(tensor owning memory, pointer, row stride) for [R,3] direction rows, allowing the
+    [R,6]-ray slice view rays[:, 3:6] without a copy."""
+    if rays_d.dim() == 2 and rays_d.shape[1] == 3 and rays_d.stride(1) == 1 and rays_d.dtype == torch.float32:
+        return rays_d, rays_d.data_ptr(), rays_d.stride(0)
+    c = _f32c(rays_d.reshape(-1, 3), "rays_d")
+    return c, c.data_ptr(), 3
+
+
+class _Composite(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, raw, z, rays_d, white):
+        raw, z = _f32c(raw, "raw"), _f32c(z, "z")
+        R, S = z.shape
+        keep, dptr, dstride = _dirs_view(rays_d)
+        dev = raw.device
+        rgb = torch.empty(R, 3, device=dev, dtype=torch.float32)
+        depth = torch.empty(R, device=dev, dtype=torch.float32)
+        acc = torch.empty(R, device=dev, dtype=torch.float32)
+        w = torch.empty(R, S, device=dev, dtype=torch.float32)
+        check(lib().nerf_composite_fwd(ptr(raw), ptr(z), dptr, dstride, R, S, int(bool(white)), ptr(rgb), ptr(depth),
+                                       ptr(acc), ptr(w), stream_of(raw)), "nerf_composite_fwd")
+        ctx.save_for_backward(raw, z, keep)
+        ctx.dptr, ctx.dstride, ctx.white = dptr, dstride, int(bool(white))
+        ctx.mark_non_differentiable(w)
+        return rgb, depth, acc, w
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_depth, g_acc, g_w):
+        raw, z, _keep = ctx.saved_tensors
+        R, S = z.shape
+        if g_rgb is None:
+            g_rgb = torch.zeros(R, 3, device=raw.device, dtype=torch.float32)
+        g_rgb = g_rgb.contiguous()
+        g_depth = None if g_depth is None else g_depth.contiguous()
+        g_acc = None if g_acc is None else g_acc.contiguous()
+        g_raw = torch.empty_like(raw)
+        check(lib().nerf_composite_bwd(ptr(raw), ptr(z), ctx.dptr, ctx.dstride, R, S, ctx.white, ptr(g_rgb),
+                                       ptr(g_depth), ptr(g_acc), ptr(g_raw), stream_of(raw)), "nerf_composite_bwd")
+        return g_raw, None, None, None
+
+
+def composite(raw: torch.Tensor, z: torch.Tensor, rays_d: torch.Tensor, white_bkgd: bool = True):
+    """raw2outputs: -> rgb [R,3], depth [R], acc [R], weights [R,S] (weights carry no grad)."""
+    return _Composite.apply(raw.reshape(z.shape[0], z.shape[1], 4), z, rays_d, white_bkgd)
+
+
+# --------------------------------------------------------------------------------------
+# MLP (autograd)
+# --------------------------------------------------------------------------------------
+NET_PARAM_NAMES = (
+    [f"pts_linears.{i}.{k}" for i in range(8) for k in ("weight", "bias")]
+    + [f"{n}.{k}" for n in ("views_linears.0", "feature_linear", "alpha_linear", "rgb_linear")
+       for k in ("weight", "bias")]
+)
+
+
+_PARAM_GENERATION = [0]
+
+
+def params_updated() -> None:
+    """Invalidate every packed-weight cache: call after parameters were written by a kernel
+    torch does not see (the fused Adam step bypasses torch's version counters)."""
+    _PARAM_GENERATION[0] += 1
+
+
+class PackedMLP:
+    """Re-packs one NeRF's 24 fp32 parameters into the kernels' lane-linear layout,
+    lazily, whenever a parameter changed (version counter / storage)."""
+
+    def __init__(self, params: Sequence[torch.Tensor]):
+        if len(params) != 24:
+            raise ValueError("expected the 24 parameters of one NeRF in state_dict order")
+        self.params = list(params)
+        self._cache = {}
+
+    def _key(self):
+        return (_PARAM_GENERATION[0],) + tuple((p.data_ptr(), p._version) for p in self.params)
+
+    def get(self, dtype: int, direction: int) -> torch.Tensor:
+        key = self._key()
+        ent = self._cache.get((dtype, direction))
+        if ent is not None and ent[0] == key:
+            return ent[1]
+        dev = self.params[0].device
+        for p in self.params:
+            if p.dtype != torch.float32 or not p.is_contiguous() or p.device != dev:
+                raise TypeError("NeRF parameters must be contiguous float32 tensors on one device")
+        nbytes = lib().nerf_mlp_packed_bytes(dtype, direction)
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        arr = _ctypes.cast((_ctypes.c_void_p * 24)(*[p.data_ptr() for p in self.params]), _ctypes.c_void_p)
+        fwd = buf if direction == 0 else None
+        bwd = buf if direction == 1 else None
+        check(lib().nerf_mlp_pack(arr, dtype, ptr(fwd), ptr(bwd), stream_of(self.params[0])), "nerf_mlp_pack")
+        self._cache[(dtype, direction)] = (key, buf)
+        return buf
+
+
+class _MLP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pts, viewdirs, dir_index, spd, packer, dtype, density_only, want_grad, *params):
+        pts = _f32c(pts.reshape(-1, 3), "pts")
+        M = pts.shape[0]
+        dev = pts.device
+        store = bool(want_grad) and any(ctx.needs_input_grad[8:])
+        raw = torch.empty(M, 4, device=dev, dtype=torch.float32)
+        if M == 0:
+            ctx.M = 0
+            return raw
+        if viewdirs is not None:
+            viewdirs = _f32c(viewdirs.reshape(-1, 3), "viewdirs")
+        if dir_index is not None:
+            dir_index = dir_index.to(torch.int32).contiguous()
+        act = masks = None
+        flags = 0
+        if store:
+            act = torch.empty(lib().nerf_mlp_act_bytes(dtype, M), dtype=torch.uint8, device=dev)
+            masks = torch.empty(lib().nerf_mlp_mask_bytes(M), dtype=torch.uint8, device=dev)
+            flags |= 1
+        if density_only:
+            flags |= 2
+        packed = packer.get(dtype, 0)
+        with kernel_timer("mlp_fwd_train" if store else ("mlp_fwd_density" if density_only else "mlp_fwd"), M):
+            check(lib().nerf_mlp_fwd(ptr(packed), dtype, ptr(pts), ptr(viewdirs), int(spd), ptr(dir_index), M, flags,
+                                     ptr(raw), ptr(act), ptr(masks), stream_of(pts)), "nerf_mlp_fwd")
+        ctx.M, ctx.dtype, ctx.packer = M, dtype, packer
+        ctx.act, ctx.masks = act, masks
+        if store:
+            ctx.packed_bwd = packer.get(dtype, 1)
+        return raw
+
+    @staticmethod
+    def backward(ctx, g_raw):
+        params = ctx.packer.params
+        nones = (None,) * 8
+        if ctx.M == 0:
+            return nones + tuple(torch.zeros_like(p) for p in params)
+        dev = g_raw.device
+        g_raw = g_raw.contiguous()
+        dz = torch.empty(lib().nerf_mlp_dz_bytes(ctx.dtype, ctx.M), dtype=torch.uint8, device=dev)
+        grad = torch.zeros(lib().nerf_mlp_net_params(), device=dev, dtype=torch.float32)
+        s = stream_of(g_raw)
+        with kernel_timer("mlp_bwd_dx", ctx.M):
+            check(lib().nerf_mlp_bwd_dx(ptr(ctx.packed_bwd), ctx.dtype, ptr(g_raw), ctx.M, ptr(ctx.masks), ptr(dz), s),
+                  "nerf_mlp_bwd_dx")
+        with kernel_timer("mlp_bwd_dw", ctx.M):
+            check(lib().nerf_mlp_bwd_dw(ctx.dtype, ctx.M, ptr(ctx.act), ptr(dz), ptr(grad), s), "nerf_mlp_bwd_dw")
+        ctx.act = ctx.masks = None
+        out, off = [], 0
+        for p in params:
+            n = p.numel()
+            out.append(grad[off:off + n].view_as(p))
+            off += n
+        return nones + tuple(out)
+
+
+def mlp(packer: PackedMLP, pts: torch.Tensor, viewdirs: Optional[torch.Tensor], samples_per_dir: int = 1,
+        dir_index: Optional[torch.Tensor] = None, dtype=F32, density_only: bool = False) -> torch.Tensor:
+    """NeRF MLP on points [...,3] -> raw [M,4] (differentiable w.r.t. the packer's params)."""
+    want_grad = torch.is_grad_enabled() and any(p.requires_grad for p in packer.params)
+    return _MLP.apply(pts, viewdirs, dir_index, samples_per_dir, packer, dtype_code(dtype), density_only, want_grad,
+                      *packer.params)
+
+
+# --------------------------------------------------------------------------------------
+# occupancy grid
+# --------------------------------------------------------------------------------------
+def _bbox_arr(bbox):
+    flat = [float(v) for v in bbox[0]] + [float(v) for v in bbox[1]]
+    arr = (_ctypes.c_float * 6)(*flat)
+    _keepalive.append(arr)
+    if len(_keepalive) > 64:
+        del _keepalive[:32]
+    return _ctypes.cast(arr, _ctypes.c_void_p)
+
+
+_keepalive = []
+
+
+def grid_index(pts: torch.Tensor, grid: Optional[torch.Tensor], res: int, bbox=SCENE_BBOX, want_idx: bool = True):
+    pts = _f32c(pts.reshape(-1, 3), "pts")
+    M = pts.shape[0]
+    idx = torch.empty(M, 3, dtype=torch.int64, device=pts.device) if want_idx else None
+    occ = torch.empty(M, dtype=torch.uint8, device=pts.device) if grid is not None else None
+    g = grid.to(torch.uint8).contiguous() if grid is not None else None
+    check(lib().nerf_grid_index(ptr(pts), M, _bbox_arr(bbox), res, ptr(g), ptr(idx), ptr(occ), stream_of(pts)),
+          "nerf_grid_index")
+    return idx, (occ.bool() if occ is not None else None)
+
+
+def bake_lattice_exact(res: int, bbox=SCENE_BBOX) -> bool:
+    """True when bmin + L*voxel == (bmin + (L-1)*voxel) + voxel in fp32 for every lattice L,
+    i.e. the (res+1)^3 shared-corner evaluation is bit-identical to the 8-corner one."""
+    import numpy as np
+    for k in range(3):
+        mn, mx = np.float32(bbox[0][k]), np.float32(bbox[1][k])
+        vs = np.float32(np.float32(mx - mn) / np.float32(res))
+        L = np.arange(1, res + 1, dtype=np.float32)
+        a = np.float32(mn) + (L * vs).astype(np.float32)
+        b = (np.float32(mn) + ((L - 1) * vs).astype(np.float32)).astype(np.float32) + vs
+        if not np.array_equal(a.astype(np.float32), b.astype(np.float32)):
+            return False
+    return True
+
+
+def bake(packer: PackedMLP, res: int, threshold: float, bbox=SCENE_BBOX, dtype=F32, device=None,
+         dedup: Optional[bool] = None, return_sigma: bool = False):
+    """Occupancy grid bake -> bool [res,res,res] (occupancy_grid.py:15-80)."""
+    device = device or packer.params[0].device
+    if dedup is None:
+        dedup = bake_lattice_exact(res, bbox)
+    P = lib().nerf_bake_num_points(res, int(dedup))
+    pts = torch.empty(P, 3, device=device, dtype=torch.float32)
+    s = stream_of(pts)
+    check(lib().nerf_bake_points(res, _bbox_arr(bbox), int(dedup), ptr(pts), s), "nerf_bake_points")
+    with torch.no_grad():
+        raw = mlp(packer, pts, None, 1, None, dtype, density_only=True)
+    grid = torch.empty(res, res, res, device=device, dtype=torch.uint8)
+    check(lib().nerf_bake_reduce(ptr(raw), res, int(dedup), float(threshold), ptr(grid), s), "nerf_bake_reduce")
+    if return_sigma:
+        return grid.bool(), raw[:, 3].clamp_min(0), pts
+    return grid.bool()
+
+
+def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: torch.Tensor, step_size: float = 0.005,
+          t_thresh: float = 1e-4, bbox=SCENE_BBOX, white_bkgd: bool = True, dtype=F32,
+          t_table: Optional[torch.Tensor] = None, k_schedule=(16, 32, 64, 128, 256, 512, 1024)):
+    """Grid-accelerated march with early termination -> dict(rgb_map_f, depth_map_f,
+    acc_map_f, n_queried, rounds)."""
+    rays = _f32c(rays.reshape(-1, 6), "rays")
+    dev, N = rays.device, rays.shape[0]
+    L = lib()
+    s = stream_of(rays)
+    if t_table is None:
+        t_table = device_table("arange", float(near), float(far), float(step_size), dev)
+    t_table = _f32c(t_table.to(dev), "t_table")
+    n_steps = t_table.numel()
+    g = grid.to(device=dev, dtype=torch.uint8).contiguous()
+    res = grid.shape[0]
+    T = torch.empty(N, device=dev)
+    rgb = torch.empty(N, 3, device=dev)
+    depth = torch.empty(N, device=dev)
+    acc = torch.empty(N, device=dev)
+    nxt = torch.empty(N, dtype=torch.int32, device=dev)
+    alive = torch.empty(N, dtype=torch.uint8, device=dev)
+    exh = torch.empty(N, dtype=torch.uint8, device=dev)
+    start = torch.empty(N, dtype=torch.int32, device=dev)
+    off = torch.empty(N, dtype=torch.int32, device=dev)
+    cnt = torch.empty(N, dtype=torch.int32, device=dev)
+    counters = torch.zeros(2, dtype=torch.int32, device=dev)
+    # unit view directions of every ray (d / |d|), as render_accelerated computes per query
+    _, _, vd = sample_stratified(rays, near, far, 1, False, want_pts=False)
+    check(L.nerf_march_init(ptr(T), ptr(rgb), ptr(depth), ptr(acc), ptr(nxt), ptr(alive), ptr(exh), N, s),
+          "nerf_march_init")
+    bb = _bbox_arr(bbox)
+    queried, rounds, ki = 0, 0, 0
+    while True:
+        K = k_schedule[min(ki, len(k_schedule) - 1)]
+        cap = N * K
+        out_ray = torch.empty(cap, dtype=torch.int32, device=dev)
+        out_step = torch.empty(cap, dtype=torch.int32, device=dev)
+        out_pts = torch.empty(cap, 3, device=dev)
+        counters.zero_()
+        check(L.nerf_march_gather(ptr(rays), N, ptr(t_table), n_steps, ptr(g), res, bb, K, ptr(T), ptr(rgb),
+                                  ptr(depth), ptr(acc), ptr(nxt), ptr(alive), ptr(exh), ptr(counters), ptr(start),
+                                  ptr(out_ray), ptr(out_step), ptr(out_pts), ptr(off), ptr(cnt), cap, s),
+              "nerf_march_gather")
+        n_pts, n_alive = (int(v) for v in counters.tolist())
+        if n_alive == 0:
+            break
+        rounds += 1
+        raw = torch.empty(0, 4, device=dev)
+        if n_pts > 0:
+            with torch.no_grad():
+                raw = mlp(packer, out_pts[:n_pts], vd, 1, out_ray[:n_pts], dtype)
+            queried += n_pts
+        check(L.nerf_march_composite(ptr(raw), ptr(rays), N, ptr(t_table), ptr(off), ptr(cnt), ptr(out_step), ptr(T),
+                                     ptr(rgb), ptr(depth), ptr(acc), ptr(nxt), ptr(alive), ptr(exh),
+                                     float(step_size), float(t_thresh), s), "nerf_march_composite")
+        ki += 1
+    check(L.nerf_march_finish(ptr(rgb), ptr(acc), N, int(bool(white_bkgd)), s), "nerf_march_finish")
+    return {"rgb_map_f": rgb, "depth_map_f": depth, "acc_map_f": acc, "n_queried": queried, "rounds": rounds}
+
+
+# --------------------------------------------------------------------------------------
+# optimizer
+# --------------------------------------------------------------------------------------
+def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, lr: float,
+              step: int, betas=(0.9, 0.999), eps: float = 1e-8, clip_value: float = 0.0):
+    """Fused clip_grad_value_ + Adam over flat contiguous fp32 buffers (in place)."""
+    for t in (param, grad, exp_avg, exp_avg_sq):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise TypeError("adam_step needs contiguous float32 buffers")
+    check(lib().nerf_adam_step(ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(), float(lr),
+                               float(betas[0]), float(betas[1]), float(eps), int(step), float(clip_value),
+                               stream_of(param)), "nerf_adam_step")
+
+
+def param_list(module: torch.nn.Module) -> List[torch.Tensor]:
+    """The 24 parameters of one NeRF module in the kernel's (state_dict) order."""
+    sd = dict(module.named_parameters())
+    return [sd[n] for n in NET_PARAM_NAMES]

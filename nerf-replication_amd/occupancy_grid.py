@@ -1,0 +1,47 @@
+"""Occupancy-grid bake / "grid update" (reference: occupancy_grid.py:15-80).
+
+    python occupancy_grid.py --cfg_file configs/nerf/lego.yaml
+
+sigma = relu(coarse raw[3]) at the 8 corners of each of res^3 voxels, occupied if any
+corner has sigma > threshold; saved as a bool [res,res,res] tensor to
+logs/<cfg name>/occupancy_grid.pt.  On the GPU the corners shared by neighbouring voxels
+are evaluated once ((res+1)^3 points instead of 8 res^3, bit-identical because the lego
+corner coordinates are exact in fp32) by the density-only fused MLP.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+
+from src.config import cfg, args  # noqa: E402
+from src.config.config import apply_gpus  # noqa: E402
+
+
+def main():
+    from nerf_amd import ops
+    from src.models import make_network
+    from src.utils.net_utils import load_network
+
+    apply_gpus(cfg)
+    network = make_network(cfg).cuda()
+    load_network(network, cfg.trained_model_dir, epoch=cfg.test.epoch)
+    network.eval()
+    res = int(cfg.task_arg.occupancy_grid_res)
+    thr = float(cfg.task_arg.occupancy_grid_threshold)
+    b = cfg.train_dataset.scene_bbox
+    bbox = (tuple(map(float, b[0])), tuple(map(float, b[1])))
+    with torch.no_grad():
+        grid = ops.bake(network.model.packer(), res, thr, bbox, dtype=network.mlp_dtype)
+    name = os.path.splitext(os.path.basename(args.cfg_file))[0]
+    out_dir = os.path.join("logs", name)
+    os.makedirs(out_dir, exist_ok=True)
+    path = os.path.join(out_dir, "occupancy_grid.pt")
+    print(f"Saving occupancy grid to: {path}")
+    torch.save(grid.cpu(), path)
+    print("Done.")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,84 @@
+"""Drop-in ``evaluator_module`` (reference: src/evaluators/nerf.py:16-92).
+
+PSNR on the float images (nerf.py:23-26) and SSIM on uint8 images with
+data_range = pred.max() - pred.min() (nerf.py:28-45).  scikit-image is not installed in
+this image, so ``structural_similarity`` is restated from its documented defaults
+(7x7 uniform window via scipy.ndimage.uniform_filter in 'reflect' mode, K1 = 0.01,
+K2 = 0.03, sample covariance N/(N-1), border of 3 px cropped before the mean, mean over
+channels).  Parity of this restatement with scikit-image is unpinned here (no skimage
+to compare against).  PNG dumps use PIL instead of cv2.
+"""
+import json
+import os
+
+import numpy as np
+from scipy.ndimage import uniform_filter
+
+from src.config import cfg
+
+
+def psnr_metric(pred, gt):
+    mse = np.mean((pred - gt) ** 2)
+    return -10 * np.log(mse) / np.log(10)
+
+
+def ssim_channel(x, y, data_range, win=7, K1=0.01, K2=0.03):
+    x = x.astype(np.float64)
+    y = y.astype(np.float64)
+    ux, uy = uniform_filter(x, size=win), uniform_filter(y, size=win)
+    uxx, uyy, uxy = uniform_filter(x * x, size=win), uniform_filter(y * y, size=win), uniform_filter(x * y, size=win)
+    n = win ** 2
+    cov = n / (n - 1.0)
+    vx, vy, vxy = cov * (uxx - ux * ux), cov * (uyy - uy * uy), cov * (uxy - ux * uy)
+    C1, C2 = (K1 * data_range) ** 2, (K2 * data_range) ** 2
+    S = ((2 * ux * uy + C1) * (2 * vxy + C2)) / ((ux ** 2 + uy ** 2 + C1) * (vx + vy + C2))
+    pad = (win - 1) // 2
+    return S[pad:-pad, pad:-pad].mean()
+
+
+def ssim_metric_uint8(pred_u8, gt_u8):
+    data_range = float(pred_u8.max()) - float(pred_u8.min())
+    return float(np.mean([ssim_channel(pred_u8[..., c], gt_u8[..., c], data_range) for c in range(pred_u8.shape[-1])]))
+
+
+class Evaluator:
+    def __init__(self):
+        self.mse, self.psnr, self.ssim = [], [], []
+        self.save_images = cfg.get("save_result", True)
+
+    def psnr_metric(self, img_pred, img_gt):
+        return psnr_metric(img_pred, img_gt)
+
+    def ssim_metric(self, img_pred, img_gt, batch, id, num_imgs):
+        if self.save_images:
+            from PIL import Image
+            d = os.path.join(cfg.result_dir, "images")
+            os.makedirs(d, exist_ok=True)
+            Image.fromarray(np.clip(img_pred * 255, 0, 255).astype(np.uint8)).save(f"{d}/view{id:03d}_pred.png")
+            Image.fromarray(img_gt).save(f"{d}/view{id:03d}_gt.png")
+        return ssim_metric_uint8((img_pred * 255).astype(np.uint8), img_gt)
+
+    def evaluate(self, output, batch):
+        pred = output["rgb_map_f"].detach().float().cpu().numpy()
+        gt = batch["rgbs"].detach().float().cpu().numpy().reshape(-1, 3)
+        i = int(batch["i"].reshape(-1)[0])
+        H, W = int(batch["H"].reshape(-1)[0]), int(batch["W"].reshape(-1)[0])
+        img_pred, img_gt = pred.reshape(H, W, 3), gt.reshape(H, W, 3)
+        psnr = self.psnr_metric(img_pred, img_gt)
+        ssim = self.ssim_metric(img_pred, (img_gt * 255).astype(np.uint8), batch, i, 100)
+        self.psnr.append(psnr)
+        self.ssim.append(ssim)
+        return {"psnr": psnr, "ssim": ssim}
+
+    def summarize(self):
+        mean_psnr, mean_ssim = float(np.mean(self.psnr)), float(np.mean(self.ssim))
+        print("Final Evaluation Results:")
+        print(f"  Average PSNR: {mean_psnr:.4f}")
+        print(f"  Average SSIM: {mean_ssim:.4f}")
+        os.makedirs(cfg.result_dir, exist_ok=True)
+        path = os.path.join(cfg.result_dir, "summary.json")
+        with open(path, "w") as f:
+            json.dump({"mean_psnr": mean_psnr, "mean_ssim": mean_ssim}, f, indent=4)
+        print(f"\nSummary saved to {path}")
+        self.psnr, self.ssim = [], []
+        return {"psnr": mean_psnr, "ssim": mean_ssim}
