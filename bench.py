@@ -50,6 +50,19 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(kernel, dtype):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/r*/traffic.json, written by tools/pmc_traffic.py from rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("dtype") == dtype and kernel in d.get("kernels", {}):
+            return d["kernels"][kernel]["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -133,7 +146,7 @@ def cpu_baseline(n_rays):
 
     once()
     t0 = time.perf_counter()
-    reps = 2
+    reps = 5
     for _ in range(reps):
         once()
     dt = (time.perf_counter() - t0) / reps
@@ -176,6 +189,7 @@ def main():
     avg_ms = ms / n_launch
     flop_per_launch = FLOP_PER_SAMPLE.get(name, 0) * units / n_launch
     achieved = flop_per_launch / (avg_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(name, args.dtype)
     kt = {k: {"launches": n, "avg_ms": round(m / n, 4), "samples_per_launch": u // n,
               "tflops": round(FLOP_PER_SAMPLE.get(k, 0) * (u / n) / (m / n * 1e-3) / 1e12, 2)}
           for k, (n, m, u) in ktimes.items()}
@@ -199,7 +213,8 @@ def main():
                        "samples_per_ray": 64 + 192, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2),
                          "peak": PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_TFLOPS[args.dtype], 4), "traffic": None,
+                         "frac": round(achieved / PEAK_TFLOPS[args.dtype], 4), "traffic": traffic,
+                         "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
                          "flop_per_launch": flop_per_launch, "avg_launch_ms": round(avg_ms, 4)},
             "kernels": kt,
             "render_s_per_frame": None if render_s is None else round(render_s, 4),

@@ -57,6 +57,10 @@ struct PF32 {
   static __device__ __forceinline__ float lsum(uint4 a) {
     return ((__uint_as_float(a.x) + __uint_as_float(a.y)) + __uint_as_float(a.z)) + __uint_as_float(a.w);
   }
+  static __device__ __forceinline__ uint4 chunk(const Tile& t, int c) {
+    return make_uint4(__float_as_uint(t.v[4 * c]), __float_as_uint(t.v[4 * c + 1]), __float_as_uint(t.v[4 * c + 2]),
+                      __float_as_uint(t.v[4 * c + 3]));
+  }
 };
 
 struct PBF16 {
@@ -84,6 +88,7 @@ struct PBF16 {
     for (int i = 0; i < 8; ++i) s += (float)v[i];
     return s;
   }
+  static __device__ __forceinline__ uint4 chunk(const Tile& t, int c) { return __builtin_bit_cast(uint4, t.b[c]); }
 };
 
 template <class P> __host__ __device__ constexpr int samples_per_block() { return P::WAVES * 32; }
@@ -164,6 +169,15 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)lds_wave_base, 16, 0, 0);
 }
 
+// The same LDS-DMA hidden from hipcc's waitcnt bookkeeping: hipcc waits vmcnt(0) before
+// any ds_read_tr while one of its own LDS-DMAs is pending, which would drain a multi-block
+// ring.  The caller owns completion (counted s_waitcnt vmcnt + s_barrier before reading).
+__device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t lds_wave_base) {
+  uint32_t saved;  // m0 is reserved to the compiler: save and restore it around the DMA
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(saved) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_wave_base)) : "memory");
+}
+
 template <class P, int SLOT_CHUNKS>
 struct Stream {
   const uint4* g;  // chunk c of the packed buffer starts at g + 64 c
@@ -214,13 +228,14 @@ __device__ __forceinline__ void pe_tile(typename P::Tile& t, int tile, int nfreq
   }
 }
 
-// feature-major stores: row (row0 + acc_row(rho, h)), column m
+// fragment-native store of one finished tile (mlp_tables.h, "Training stores"): CH
+// lane-linear 16-byte stores per lane, each wave-instruction writes 1 KiB contiguous
 template <class P>
-__device__ __forceinline__ void store_tile(void* base, int64_t ldm, int row0, int64_t m, int h,
+__device__ __forceinline__ void store_tile(void* base, int64_t nblk, int tau, int64_t wblock, int lane,
                                            const typename P::Tile& t) {
-  typename P::Store* b = (typename P::Store*)base;
+  uint4* dst = (uint4*)base + ((int64_t)tau * nblk + wblock) * P::CH * 64 + lane;
 #pragma unroll
-  for (int rho = 0; rho < 16; ++rho) b[(int64_t)(row0 + acc_row(rho, h)) * ldm + m] = P::cvt(P::get(t, rho));
+  for (int c = 0; c < P::CH; ++c) dst[c * 64] = P::chunk(t, c);
 }
 
 struct FwdArgs {
@@ -230,15 +245,15 @@ struct FwdArgs {
   const int32_t* dir_index;  // [M] or null (then dir = m / samples_per_dir)
   int samples_per_dir;
   int64_t M;
-  int64_t ldm;               // row stride of act (M padded to M_ALIGN)
+  int64_t nblk;              // 32-sample blocks of the stores (M padded to M_ALIGN) / 32
   float* raw;                // [M,4]
-  void* act;                 // [A_ROWS, ldm] or null
-  uint16_t* masks;           // [ldm/32, MASK_TILES, 64] or null
+  void* act;                 // [AT_TILES][nblk] tile-blocks or null
+  uint16_t* masks;           // [nblk, MASK_TILES, 64] or null
 };
 
 // activation of a finished accumulator tile -> next layer's B operand (+ training stores)
 template <class P, bool RELU, bool STORE>
-__device__ __forceinline__ void finish_tile(const f32x16& acc, typename P::Tile& out, const FwdArgs& a, int act_row,
+__device__ __forceinline__ void finish_tile(const f32x16& acc, typename P::Tile& out, const FwdArgs& a, int act_tile,
                                             int mask_tile, int64_t m, int64_t wblock, int h, int lane) {
   uint32_t mask = 0;
 #pragma unroll
@@ -251,7 +266,7 @@ __device__ __forceinline__ void finish_tile(const f32x16& acc, typename P::Tile&
     P::set(out, rho, x);
   }
   if (STORE) {
-    store_tile<P>(a.act, a.ldm, act_row, m, h, out);
+    store_tile<P>(a.act, a.nblk, act_tile, wblock, lane, out);
     if (RELU) a.masks[(wblock * MASK_TILES + mask_tile) * 64 + lane] = (uint16_t)mask;
   }
 }
@@ -325,9 +340,9 @@ __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
     if (STORE) {
       Tile D;
       pe_tile<P>(D, 0, 4, 27, h, dx, dy, dz);
-      store_tile<P>(a.act, a.ldm, A_X, m, h, X[0]);
-      store_tile<P>(a.act, a.ldm, A_X + 32, m, h, X[1]);
-      store_tile<P>(a.act, a.ldm, A_D, m, h, D);
+      store_tile<P>(a.act, a.nblk, AT_X, wblock, lane, X[0]);
+      store_tile<P>(a.act, a.nblk, AT_X + 1, wblock, lane, X[1]);
+      store_tile<P>(a.act, a.nblk, AT_D, wblock, lane, D);
     }
     __syncthreads();
     int unit = 0;
@@ -338,7 +353,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
       acc = tile_mma<P>(ws.cur(), 0, X[0], acc, lane);
       acc = tile_mma<P>(ws.cur(), 1, X[1], acc, lane);
       end();
-      finish_tile<P, true, STORE>(acc, Ha[n], a, A_H + 32 * n, n, m, wblock, h, lane);
+      finish_tile<P, true, STORE>(acc, Ha[n], a, AT_H + n, n, m, wblock, h, lane);
     }
   }
   int unit = 8;
@@ -348,7 +363,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
     begin(unit);                                                                                 \
     _Pragma("unroll") for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), t, IN[t], acc, lane); \
     end();                                                                                       \
-    finish_tile<P, true, STORE>(acc, OUT[n], a, A_H + (L) * 256 + 32 * n, (L) * 8 + n, m, wblock, h, lane); \
+    finish_tile<P, true, STORE>(acc, OUT[n], a, AT_H + (L) * 8 + n, (L) * 8 + n, m, wblock, h, lane);     \
   }
   NERF_HIDDEN_LAYER(1, Ha, Hb)
   NERF_HIDDEN_LAYER(2, Hb, Ha)
@@ -367,7 +382,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), 2 + t, Ha[t], acc, lane);
       end();
-      finish_tile<P, true, STORE>(acc, Hb[n], a, A_H + 5 * 256 + 32 * n, 5 * 8 + n, m, wblock, h, lane);
+      finish_tile<P, true, STORE>(acc, Hb[n], a, AT_H + 5 * 8 + n, 5 * 8 + n, m, wblock, h, lane);
     }
   }
   NERF_HIDDEN_LAYER(6, Hb, Ha)
@@ -381,7 +396,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), t, Hb[t], acc, lane);
       end();
-      finish_tile<P, false, STORE>(acc, Ha[n], a, A_F + 32 * n, 0, m, wblock, h, lane);
+      finish_tile<P, false, STORE>(acc, Ha[n], a, AT_F + n, 0, m, wblock, h, lane);
     }
   } else {
     unit += 8;
@@ -410,7 +425,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
       for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), t, Ha[t], acc, lane);
       acc = tile_mma<P>(ws.cur(), 8, D, acc, lane);
       end();
-      finish_tile<P, true, STORE>(acc, Hb[n], a, A_V + 32 * n, 64 + n, m, wblock, h, lane);
+      finish_tile<P, true, STORE>(acc, Hb[n], a, AT_V + n, 64 + n, m, wblock, h, lane);
     }
   }
   // ---- rgb (rows 0..2: lanes 0..31, registers 0..2)
@@ -427,18 +442,18 @@ __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
 struct DxArgs {
   const char* wpack_t;  // W^T chunks
   const float* d_raw;   // [M,4]
-  int64_t M, ldm;
+  int64_t M, nblk;
   const uint16_t* masks;
-  void* dz;             // [Z_ROWS, ldm]
+  void* dz;             // [ZT_TILES][nblk] tile-blocks
 };
 
 template <class P, bool MASK>
-__device__ __forceinline__ void dx_finish(const f32x16& acc, typename P::Tile& out, const DxArgs& a, int dz_row,
+__device__ __forceinline__ void dx_finish(const f32x16& acc, typename P::Tile& out, const DxArgs& a, int dz_tile,
                                           int mask_tile, int64_t m, int64_t wblock, int h, int lane) {
   const uint32_t mask = MASK ? (uint32_t)a.masks[(wblock * MASK_TILES + mask_tile) * 64 + lane] : 0xFFFFu;
 #pragma unroll
   for (int rho = 0; rho < 16; ++rho) P::set(out, rho, ((mask >> rho) & 1u) ? acc[rho] : 0.f);
-  store_tile<P>(a.dz, a.ldm, dz_row, m, h, out);
+  store_tile<P>(a.dz, a.nblk, dz_tile, wblock, lane, out);
 }
 
 template <class P>
@@ -473,8 +488,8 @@ __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
     P::set(G, rho, (h == 0 && rho < 3) ? (rho == 0 ? g.x : rho == 1 ? g.y : g.z) : 0.f);
     P::set(DA, rho, (h == 0 && rho == 0) ? g.w : 0.f);
   }
-  store_tile<P>(a.dz, a.ldm, Z_RGB, m, h, G);
-  store_tile<P>(a.dz, a.ldm, Z_A, m, h, DA);
+  store_tile<P>(a.dz, a.nblk, ZT_RGB, wblock, lane, G);
+  store_tile<P>(a.dz, a.nblk, ZT_A, wblock, lane, DA);
   __syncthreads();
 
   Tile Ha[8], Hb[8];
@@ -485,7 +500,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
     begin(unit);
     acc = tile_mma<P>(ws.cur(), 0, G, acc, lane);
     end();
-    dx_finish<P, true>(acc, Hb[j], a, Z_V + 32 * j, 64 + j, m, wblock, h, lane);
+    dx_finish<P, true>(acc, Hb[j], a, ZT_V + j, 64 + j, m, wblock, h, lane);
   }
   // bV: dfeature = W_v[:, :256]^T dZv -> Ha
 #pragma unroll
@@ -494,7 +509,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc = tile_mma<P>(ws.cur(), t, Hb[t], acc, lane);
     end();
-    dx_finish<P, false>(acc, Ha[j], a, Z_F + 32 * j, 0, m, wblock, h, lane);
+    dx_finish<P, false>(acc, Ha[j], a, ZT_F + j, 0, m, wblock, h, lane);
   }
   // bFA: dh7 = W_f^T dfeature + W_a^T dalpha, masked by h7 -> dZ7 (Hb)
 #pragma unroll
@@ -504,7 +519,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
     for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), t, Ha[t], acc, lane);
     acc = tile_mma<P>(ws.cur(), 8, DA, acc, lane);
     end();
-    dx_finish<P, true>(acc, Hb[j], a, Z_H + 7 * 256 + 32 * j, 7 * 8 + j, m, wblock, h, lane);
+    dx_finish<P, true>(acc, Hb[j], a, ZT_H + 7 * 8 + j, 7 * 8 + j, m, wblock, h, lane);
   }
   // b_l (l = 7..1): dh_{l-1} = W_l^T dZ_l (L5: h4 columns only), masked by h_{l-1}
 #define NERF_BWD_LAYER(L, IN, OUT)                                                                \
@@ -512,7 +527,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
     begin(unit);                                                                                  \
     _Pragma("unroll") for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), t, IN[t], acc, lane); \
     end();                                                                                        \
-    dx_finish<P, true>(acc, OUT[j], a, Z_H + ((L) - 1) * 256 + 32 * j, ((L) - 1) * 8 + j, m, wblock, h, lane); \
+    dx_finish<P, true>(acc, OUT[j], a, ZT_H + ((L) - 1) * 8 + j, ((L) - 1) * 8 + j, m, wblock, h, lane);       \
   }
   NERF_BWD_LAYER(7, Hb, Ha)
   NERF_BWD_LAYER(6, Ha, Hb)
@@ -525,17 +540,19 @@ __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
-// dW / db: C[n][k] += sum_m dz[n][m] act[k][m] over a chunk of samples.
-// job = (gemm g, n-group, k-group, sample chunk); wave w owns n-tile w of the group and
-// accumulates all (<= 8) k-tiles of the group; the act panel is shared through LDS.
+// dW / db: C[n][k] += sum_m dz[n][m] act[k][m] over a chunk of 32-sample blocks.
+// job = (gemm g, n-group, k-group, block chunk); wave w owns n-tile w of the group and
+// accumulates all (<= 8) k-tiles of the group.  Per block, the group's dz and act
+// tile-blocks (fragment-native, mlp_tables.h) are copied to LDS with global_load_lds and
+// read back transposed: K = samples.  Row i of a fragment <-> feature acc_row(i&15, i>>4).
 // ------------------------------------------------------------------------------------
 struct DwArgs {
   const void* dz;
   const void* act;
-  int64_t ldm;    // padded sample count (row stride)
-  int64_t chunk;  // samples per job (multiple of 256)
+  int64_t nblk;       // 32-sample blocks in the stores
+  int64_t chunk_blk;  // blocks per job
   int nchunks;
-  float* grad;    // flat [NET_PARAMS], accumulated
+  float* grad;        // flat [NET_PARAMS], accumulated
 };
 
 struct DwJob { int g, ng, kg; };
@@ -557,15 +574,52 @@ __device__ __forceinline__ DwJob dw_job(int j) {
 }
 
 constexpr int DW_WAVES = 8;
-constexpr int DW_LOADS = 4;  // 16-B lane loads per operand row per pipeline step
+constexpr int DW_SLOTS = 16;  // 8 dz tiles + 8 act tiles per block
+__host__ __device__ constexpr int perm_row(int i) { return acc_row(i & 15, i >> 4); }
+// LDS ring depth: 3 x 32 KiB (bf16), 2 x 64 KiB (fp32) -- both within 160 KiB
+template <class P> __host__ __device__ constexpr int dw_nbuf() { return P::CH == 2 ? 3 : 2; }
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n in [0, 8]
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
+}
+
+typedef __attribute__((ext_vector_type(4))) short short4_t;
+typedef __attribute__((address_space(3))) short4_t lds_short4;
+
+// bf16: the 8-sample K fragment (samples 16 s + 8 h + [0, 8)) of row (lane & 31)
+__device__ __forceinline__ bf16x8 dw_frag_bf16(const char* tile, int s, int lane) {
+  const int l16 = lane & 15, G = lane >> 4;
+  const int hp = G & 1, h = G >> 1, q = l16 >> 2, pp = l16 & 3;
+  const char* base = tile + (pp >> 1) * 1024 + (pp & 1) * 8 + (16 * s + 8 * h + q + 32 * hp) * 16;
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)base);
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(base + 4 * 16));
+  typedef __attribute__((ext_vector_type(8))) short short8_t;
+  short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+// fp32: the K = 2 fragment (sample 2 s + h) of row (lane & 31)
+__device__ __forceinline__ float dw_frag_f32(const char* tile, int s, int lane) {
+  const int rho = lane & 15, hp = (lane >> 4) & 1, h = lane >> 5;
+  return *(const float*)(tile + (rho >> 2) * 1024 + (2 * s + h + 32 * hp) * 16 + (rho & 3) * 4);
+}
 
 template <class P>
 __global__ void __launch_bounds__(DW_WAVES * 64) dw_kernel(DwArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
-  constexpr int SPS = 2 * P::SPL * DW_LOADS;  // samples per step
-  constexpr int BUF_U4 = DW_LOADS * 8 * 64;
+  constexpr int TB = P::CH * 1024;           // tile-block bytes
+  constexpr int BUF = DW_SLOTS * TB;         // one block's tiles
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 5, r = lane & 31;
   const int chunk_id = blockIdx.x % a.nchunks;
   const DwJob job = dw_job(blockIdx.x / a.nchunks);
   const int g = job.g;
@@ -573,15 +627,36 @@ __global__ void __launch_bounds__(DW_WAVES * 64) dw_kernel(DwArgs a) {
   const int ntiles = min(8, gemm_n_tiles(g) - nt0);
   const int ktiles = min(8, gemm_k_tiles(g) - kt0);
   const bool active = wave < ntiles;
-  const int64_t m_begin = (int64_t)chunk_id * a.chunk;
-  const int64_t m_end = min(m_begin + a.chunk, a.ldm);
-  const int64_t row_bytes = a.ldm * P::ESIZE;
+  const int64_t b_begin = (int64_t)chunk_id * a.chunk_blk;
+  const int64_t b_end = min(b_begin + a.chunk_blk, a.nblk);
+  char* lds = (char*)smem_u4;
 
-  // A operand: dz rows of this wave's n-tile; lane (r, h) reads row r, samples [SPL h, SPL h + SPL)
-  const char* arow = (const char*)a.dz + (int64_t)(gemm_dz_row(g) + 32 * (nt0 + (active ? wave : 0)) + r) * row_bytes;
-  // B operand: wave w loads k-tile w of the group into LDS (lane-linear), same lane->sample map
-  const bool bload = wave < ktiles;
-  const char* brow = (const char*)a.act + (int64_t)(gemm_act_row(g, kt0 + (bload ? wave : 0)) + r) * row_bytes;
+  // copy one block's tile-blocks into buffer `buf` (each wave-instruction = 1 KiB).  Wave w
+  // issues chunks k = w, w + 8, ... (G of them); their sources and LDS offsets are resolved
+  // once here -- a table lookup inside the loop would be an ordinary global load, whose
+  // compiler wait is vmcnt(0) and drains the ring.
+  const int nchunk = (ntiles + ktiles) * P::CH;
+  constexpr int GMAX = 16 * P::CH / DW_WAVES;
+  const int G = wave < nchunk ? (nchunk - wave + DW_WAVES - 1) / DW_WAVES : 0;
+  const char* src[GMAX];
+  int dst[GMAX];
+#pragma unroll
+  for (int i = 0; i < GMAX; ++i) {
+    const int k = wave + DW_WAVES * i;
+    const int which = k / P::CH, c = k % P::CH;
+    const bool is_a = which < ntiles;
+    const int slot = is_a ? which : 8 + (which - ntiles);
+    const int tau = k >= nchunk ? 0 : is_a ? gemm_dz_tile(g, nt0 + which) : gemm_act_tile(g, kt0 + which - ntiles);
+    src[i] = (const char*)(is_a ? a.dz : a.act) + ((int64_t)tau * a.nblk * P::CH + c) * 1024 + lane * 16;
+    dst[i] = slot * TB + c * 1024;
+  }
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_void*)lds;
+  auto fetch = [&](int64_t b, int buf) {
+    const int64_t boff = b * (P::CH * 1024);
+#pragma unroll
+    for (int i = 0; i < GMAX; ++i)
+      if (i < G) glds16_asm(src[i] + boff, lds_base + buf * BUF + dst[i]);
+  };
 
   f32x16 acc[8];
 #pragma unroll
@@ -590,40 +665,48 @@ __global__ void __launch_bounds__(DW_WAVES * 64) dw_kernel(DwArgs a) {
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
   float dbias = 0.f;
 
-  uint4 an[DW_LOADS], ac[DW_LOADS];
-  // prologue: step 0 -> buffer 0
-#pragma unroll
-  for (int s = 0; s < DW_LOADS; ++s) {
-    const int64_t off = (m_begin + s * 2 * P::SPL + h * P::SPL) * P::ESIZE;
-    if (bload) glds16(brow + off, smem_u4 + (s * 8 + wave) * 64);
-    ac[s] = *(const uint4*)(arow + off);
-  }
-  __syncthreads();
+  // NBUF-slot ring, D = NBUF - 1 blocks in flight: per block each wave issues the same
+  // number G of global_load_lds, so "block b landed" = vmcnt(G * younger blocks in flight),
+  // then a raw s_barrier -- no vmcnt(0) drain (cdna_hip_programming.md, LDS-DMA ordering).
+  constexpr int NBUF = dw_nbuf<P>(), D = NBUF - 1;
+  for (int d = 0; d < D; ++d)
+    if (b_begin + d < b_end) fetch(b_begin + d, d);
   int buf = 0;
-  for (int64_t ms = m_begin; ms < m_end; ms += SPS) {
-    const bool more = ms + SPS < m_end;
-    if (more) {
-#pragma unroll
-      for (int s = 0; s < DW_LOADS; ++s) {
-        const int64_t off = (ms + SPS + s * 2 * P::SPL + h * P::SPL) * P::ESIZE;
-        if (bload) glds16(brow + off, smem_u4 + (buf ^ 1) * BUF_U4 + (s * 8 + wave) * 64);
-        an[s] = *(const uint4*)(arow + off);
-      }
-    }
+  for (int64_t b = b_begin; b < b_end; ++b) {
+    const int younger = (int)min((int64_t)(D - 1), b_end - 1 - b);
+    wait_vmcnt(G * younger);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (b + D < b_end) fetch(b + D, buf == 0 ? NBUF - 1 : buf - 1);
     if (active) {
-      const uint4* bp = smem_u4 + buf * BUF_U4;
+      const char* tiles = lds + buf * BUF;
+      const char* at = tiles + wave * TB;
+      if constexpr (P::CH == 2) {
 #pragma unroll
-      for (int s = 0; s < DW_LOADS; ++s) {
-        dbias += P::lsum(ac[s]);
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 af = dw_frag_bf16(at, s, lane);
 #pragma unroll
-        for (int t = 0; t < 8; ++t)
-          if (t < ktiles) acc[t] = P::mma_k(ac[s], bp[(s * 8 + t) * 64 + lane], acc[t]);
+          for (int e = 0; e < 8; ++e) dbias += (float)af[e];
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            if (t < ktiles)
+              acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, dw_frag_bf16(tiles + (8 + t) * TB, s, lane), acc[t],
+                                                               0, 0, 0);
+        }
+      } else {
+#pragma unroll 4
+        for (int s = 0; s < 16; ++s) {
+          const float af = dw_frag_f32(at, s, lane);
+          dbias += af;
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            if (t < ktiles)
+              acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af, dw_frag_f32(tiles + (8 + t) * TB, s, lane), acc[t], 0,
+                                                            0, 0);
+        }
       }
     }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < DW_LOADS; ++s) ac[s] = an[s];
-    buf ^= 1;
+    buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
   if (!active) return;
   // accumulate into the flat gradient (state_dict layout: weight [N][K] row-major)
@@ -631,22 +714,24 @@ __global__ void __launch_bounds__(DW_WAVES * 64) dw_kernel(DwArgs a) {
   float* gw = a.grad + param_offset(wp);
   const int K = weight_K(wp);
   const int nvalid = gemm_n_valid(g);
+  const int h = lane >> 5, j = lane & 31;
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     if (t < ktiles) {
       const int kt = kt0 + t;
-      const int col = gemm_col0(g, kt) + r;
-      const bool cok = r < gemm_col_valid(g, kt);
+      const int colf = perm_row(j);
+      const int col = gemm_col0(g, kt) + colf;
+      const bool cok = colf < gemm_col_valid(g, kt);
 #pragma unroll
       for (int rho = 0; rho < 16; ++rho) {
-        const int n = 32 * (nt0 + wave) + acc_row(rho, h);
+        const int n = 32 * (nt0 + wave) + perm_row(acc_row(rho, h));
         if (cok && n < nvalid) atomicAdd(gw + (int64_t)n * K + col, acc[t][rho]);
       }
     }
   }
   if (job.kg == 0) {
     dbias += __shfl_xor(dbias, 32, 64);
-    const int n = 32 * (nt0 + wave) + r;
+    const int n = 32 * (nt0 + wave) + perm_row(j);
     if (h == 0 && n < nvalid) atomicAdd(a.grad + param_offset(wp + 1) + n, dbias);
   }
 }
@@ -662,7 +747,7 @@ using namespace nerf::mlp;
 
 template <class P> static constexpr size_t fwd_lds_bytes() { return 2 * (size_t)fwd_slot_chunks<P>() * 1024; }
 template <class P> static constexpr size_t dx_lds_bytes() { return 2 * (size_t)dx_slot_chunks<P>() * 1024; }
-static constexpr size_t dw_lds_bytes() { return 2 * (size_t)DW_LOADS * 8 * 1024; }
+template <class P> static constexpr size_t dw_lds_bytes() { return (size_t)dw_nbuf<P>() * DW_SLOTS * P::CH * 1024; }
 
 template <class K>
 static void allow_lds(K kernel, size_t bytes) {
@@ -728,11 +813,11 @@ int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const floa
   NERF_REQUIRE(!store || (act && masks), "nerf_mlp_fwd: store requires act and masks");
   NERF_REQUIRE(!(store && density), "nerf_mlp_fwd: store and density-only are exclusive");
   FwdArgs a{(const char*)packed_fwd, pts, viewdirs, dir_index, samples_per_dir, M,
-            nerf_mlp_padded_samples(M), raw, act, masks};
+            nerf_mlp_padded_samples(M) / 32, raw, act, masks};
   if (dtype == 0) {
     using P = PF32;
     const int spb = samples_per_block<P>();
-    dim3 grid((unsigned)(store ? a.ldm / spb : (M + spb - 1) / spb));
+    dim3 grid((unsigned)(store ? a.nblk * 32 / spb : (M + spb - 1) / spb));
     const size_t lds = fwd_lds_bytes<P>();
     if (store) {
       allow_lds(fwd_kernel<P, true, false>, lds);
@@ -747,7 +832,7 @@ int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const floa
   } else {
     using P = PBF16;
     const int spb = samples_per_block<P>();
-    dim3 grid((unsigned)(store ? a.ldm / spb : (M + spb - 1) / spb));
+    dim3 grid((unsigned)(store ? a.nblk * 32 / spb : (M + spb - 1) / spb));
     const size_t lds = fwd_lds_bytes<P>();
     if (store) hipLaunchKernelGGL((fwd_kernel<P, true, false>), grid, dim3(P::WAVES * 64), lds, stream, a);
     else if (density) hipLaunchKernelGGL((fwd_kernel<P, false, true>), grid, dim3(P::WAVES * 64), lds, stream, a);
@@ -764,7 +849,7 @@ int64_t nerf_mlp_dw_chunk(int64_t M) {
   return ch;
 }
 
-// dX chain only: dz (per-layer output gradients, feature-major) from d_raw and the masks
+// dX chain only: dz (per-layer output gradients, fragment-native tiles) from d_raw + masks
 int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64_t M, const uint16_t* masks, void* dz,
                     hipStream_t stream) {
   NERF_REQUIRE(dtype == 0 || dtype == 1, "nerf_mlp_bwd_dx: bad dtype %d", dtype);
@@ -772,7 +857,7 @@ int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64
   if (M == 0) return 0;
   NERF_REQUIRE(packed_bwd && d_raw && masks && dz, "nerf_mlp_bwd_dx: null pointer");
   const int64_t ldm = nerf_mlp_padded_samples(M);
-  DxArgs x{(const char*)packed_bwd, d_raw, M, ldm, masks, dz};
+  DxArgs x{(const char*)packed_bwd, d_raw, M, ldm / 32, masks, dz};
   if (dtype == 0) {
     using P = PF32;
     allow_lds(dx_kernel<P>, dx_lds_bytes<P>());
@@ -792,42 +877,25 @@ int nerf_mlp_bwd_dw(int dtype, int64_t M, const void* act, const void* dz, float
   NERF_REQUIRE(M >= 0, "nerf_mlp_bwd_dw: M < 0");
   if (M == 0) return 0;
   NERF_REQUIRE(act && dz && grad, "nerf_mlp_bwd_dw: null pointer");
-  const int64_t ldm = nerf_mlp_padded_samples(M);
-  const int64_t chunk = nerf_mlp_dw_chunk(M);
-  const int nchunks = (int)((ldm + chunk - 1) / chunk);
-  DwArgs w{dz, act, ldm, chunk, nchunks, grad};
+  const int64_t nblk = nerf_mlp_padded_samples(M) / 32;
+  const int64_t chunk_blk = nerf_mlp_dw_chunk(M) / 32;
+  const int nchunks = (int)((nblk + chunk_blk - 1) / chunk_blk);
+  DwArgs w{dz, act, nblk, chunk_blk, nchunks, grad};
   dim3 grid((unsigned)(n_dw_jobs_per_chunk() * nchunks));
-  if (dtype == 0) hipLaunchKernelGGL((dw_kernel<PF32>), grid, dim3(DW_WAVES * 64), dw_lds_bytes(), stream, w);
-  else hipLaunchKernelGGL((dw_kernel<PBF16>), grid, dim3(DW_WAVES * 64), dw_lds_bytes(), stream, w);
+  if (dtype == 0) {
+    allow_lds(dw_kernel<PF32>, dw_lds_bytes<PF32>());
+    hipLaunchKernelGGL((dw_kernel<PF32>), grid, dim3(DW_WAVES * 64), dw_lds_bytes<PF32>(), stream, w);
+  } else {
+    allow_lds(dw_kernel<PBF16>, dw_lds_bytes<PBF16>());
+    hipLaunchKernelGGL((dw_kernel<PBF16>), grid, dim3(DW_WAVES * 64), dw_lds_bytes<PBF16>(), stream, w);
+  }
   return check_launch("nerf_mlp_bwd_dw");
 }
 
 int nerf_mlp_bwd(const void* packed_bwd, int dtype, const float* d_raw, int64_t M, const void* act,
                  const uint16_t* masks, void* dz, float* grad, hipStream_t stream) {
-  NERF_REQUIRE(dtype == 0 || dtype == 1, "nerf_mlp_bwd: bad dtype %d", dtype);
-  NERF_REQUIRE(M >= 0, "nerf_mlp_bwd: M < 0");
-  if (M == 0) return 0;
-  NERF_REQUIRE(packed_bwd && d_raw && act && masks && dz && grad, "nerf_mlp_bwd: null pointer");
-  const int64_t ldm = nerf_mlp_padded_samples(M);
-  DxArgs x{(const char*)packed_bwd, d_raw, M, ldm, masks, dz};
-  if (dtype == 0) {
-    using P = PF32;
-    dim3 grid((unsigned)(ldm / samples_per_block<P>()));
-    allow_lds(dx_kernel<P>, dx_lds_bytes<P>());
-    hipLaunchKernelGGL((dx_kernel<P>), grid, dim3(P::WAVES * 64), dx_lds_bytes<P>(), stream, x);
-  } else {
-    using P = PBF16;
-    dim3 grid((unsigned)(ldm / samples_per_block<P>()));
-    hipLaunchKernelGGL((dx_kernel<P>), grid, dim3(P::WAVES * 64), dx_lds_bytes<P>(), stream, x);
-  }
-  if (int e = check_launch("nerf_mlp_bwd(dx)")) return e;
-  const int64_t chunk = nerf_mlp_dw_chunk(M);
-  const int nchunks = (int)((ldm + chunk - 1) / chunk);
-  DwArgs w{dz, act, ldm, chunk, nchunks, grad};
-  dim3 grid((unsigned)(n_dw_jobs_per_chunk() * nchunks));
-  if (dtype == 0) hipLaunchKernelGGL((dw_kernel<PF32>), grid, dim3(DW_WAVES * 64), dw_lds_bytes(), stream, w);
-  else hipLaunchKernelGGL((dw_kernel<PBF16>), grid, dim3(DW_WAVES * 64), dw_lds_bytes(), stream, w);
-  return check_launch("nerf_mlp_bwd(dw)");
+  if (int e = nerf_mlp_bwd_dx(packed_bwd, dtype, d_raw, M, masks, dz, stream)) return e;
+  return nerf_mlp_bwd_dw(dtype, M, act, dz, grad, stream);
 }
 
 }  // extern "C"

@@ -127,49 +127,53 @@ __host__ __device__ constexpr int bwd_unit_tile_off(int u) {
 }
 constexpr int BWD_TILES = bwd_unit_tile_off(NUNIT_BWD);
 
-// feature-major activation store (rows x M_pad), written by the training forward
-enum ActRow {
-  A_X = 0,       // PE(xyz): 63 rows (+1 zero pad)
-  A_D = 64,      // PE(dir): 27 rows (+5 zero pad)
-  A_H = 96,      // h0..h7 post-ReLU: 8 x 256
-  A_F = 96 + 2048,  // feature (no activation): 256
-  A_V = A_F + 256,  // views hidden post-ReLU: 128
-  A_ROWS = A_V + 128  // 2528
+// Training stores, "fragment-native": a stored tensor is a list of 32-feature tiles; tile
+// tau of 32-sample block b occupies one tile-block of CH KiB at ((tau * nblk + b) * CH + c)
+// KiB (chunk c = accumulator registers [c*E, c*E+E) of every lane, lane-linear, 16 B per
+// lane) -- exactly the B-operand registers, so a wave stores a finished tile with CH
+// 16-byte stores per lane.  The dW GEMM reads them back transposed (ds_read_b64_tr_b16).
+enum ActTile {
+  AT_X = 0,    // PE(xyz): 2 tiles (63 features + 1 zero)
+  AT_D = 2,    // PE(dir): 1 tile (27 + 5 zero)
+  AT_H = 3,    // h0..h7 post-ReLU: tile 3 + 8 l + n
+  AT_F = 67,   // feature (no activation): 8 tiles
+  AT_V = 75,   // views hidden post-ReLU: 4 tiles
+  AT_TILES = 79
 };
-// feature-major output-gradient store, written by the dX chain
-enum DzRow {
-  Z_H = 0,             // dZ0..dZ7 (pre-ReLU grads of pts_linears): 8 x 256
-  Z_F = 2048,          // d feature: 256
-  Z_A = Z_F + 256,     // d alpha: row 0 of a 32-row block
-  Z_V = Z_A + 32,      // dZ views: 128
-  Z_RGB = Z_V + 128,   // d rgb: rows 0..2 of a 32-row block
-  Z_ROWS = Z_RGB + 32  // 2496
+enum DzTile {
+  ZT_H = 0,     // dZ0..dZ7 (pre-ReLU grads of pts_linears): tile 8 l + n
+  ZT_F = 64,    // d feature: 8
+  ZT_A = 72,    // d alpha: row 0 of one tile
+  ZT_V = 73,    // dZ views: 4
+  ZT_RGB = 77,  // d rgb: rows 0..2 of one tile
+  ZT_TILES = 78
 };
+constexpr int A_ROWS = AT_TILES * 32;  // 2528 feature rows
+constexpr int Z_ROWS = ZT_TILES * 32;  // 2496
 // ReLU masks: per 32-sample wave block, 68 tiles x 64 lanes x 16 bits
 constexpr int MASK_TILES = 68;  // h0..h7 (8x8), hv (4)
 
 // dW GEMM list (per net): C[n][k] = sum_m dz[n][m] act[k][m]
-//   g: (dz row base, n tiles, weight param, bias param, k tiles, act rows per k tile)
 constexpr int NGEMM = 12;
 __host__ __device__ constexpr int gemm_weight(int g) {
   return g < 8 ? 2 * g : g == 8 ? (int)P_FW : g == 9 ? (int)P_AW : g == 10 ? (int)P_VW : (int)P_RW;
 }
-__host__ __device__ constexpr int gemm_dz_row(int g) {
-  return g < 8 ? Z_H + 256 * g : g == 8 ? Z_F : g == 9 ? Z_A : g == 10 ? Z_V : Z_RGB;
+__host__ __device__ constexpr int gemm_dz_tile(int g, int nt) {
+  return g < 8 ? ZT_H + 8 * g + nt : g == 8 ? ZT_F + nt : g == 9 ? (int)ZT_A : g == 10 ? ZT_V + nt : (int)ZT_RGB;
 }
 __host__ __device__ constexpr int gemm_n_tiles(int g) { return g < 9 ? 8 : g == 9 ? 1 : g == 10 ? 4 : 1; }
-__host__ __device__ constexpr int gemm_n_valid(int g) { return g == 9 ? 1 : g == 11 ? 3 : 256; }
+__host__ __device__ constexpr int gemm_n_valid(int g) { return g == 9 ? 1 : g == 11 ? 3 : (g == 10 ? 128 : 256); }
 __host__ __device__ constexpr int gemm_k_tiles(int g) {
   return g == 0 ? 2 : g == 5 ? 10 : g == 10 ? 9 : g == 11 ? 4 : 8;
 }
-// k tile t of gemm g -> (act row base, first weight column, valid columns)
-__host__ __device__ constexpr int gemm_act_row(int g, int t) {
-  return g == 0 ? A_X + 32 * t
-       : g == 5 ? (t < 2 ? A_X + 32 * t : A_H + 256 * 4 + 32 * (t - 2))
-       : g <= 7 ? A_H + 256 * (g - 1) + 32 * t
-       : g <= 9 ? A_H + 256 * 7 + 32 * t
-       : g == 10 ? (t < 8 ? A_F + 32 * t : A_D)
-       : A_V + 32 * t;
+// k tile t of gemm g -> (act tile, first weight column, valid columns)
+__host__ __device__ constexpr int gemm_act_tile(int g, int t) {
+  return g == 0 ? AT_X + t
+       : g == 5 ? (t < 2 ? AT_X + t : AT_H + 8 * 4 + (t - 2))
+       : g <= 7 ? AT_H + 8 * (g - 1) + t
+       : g <= 9 ? AT_H + 8 * 7 + t
+       : g == 10 ? (t < 8 ? AT_F + t : (int)AT_D)
+       : AT_V + t;
 }
 __host__ __device__ constexpr int gemm_col0(int g, int t) {
   return g == 0 ? 32 * t : g == 5 ? (t < 2 ? 32 * t : 63 + 32 * (t - 2)) : 32 * t;

@@ -136,8 +136,21 @@ def main():
 
     # ---- (a3/a9) full render, 64 rays, perturb 0, and perturb 1 with injected uniforms
     batch = {"rays": rays[None, :64].clone(), "near": near, "far": far}
-    with torch.no_grad():
-        r0 = renderer.render(batch)
+    sorted_z = []
+    orig_sort = torch.sort
+
+    def spy_sort(*a, **k):  # the merged fine depths (coarse + importance samples, sorted)
+        r = orig_sort(*a, **k)
+        sorted_z.append(r[0].clone())
+        return r
+
+    torch.sort = spy_sort
+    try:
+        with torch.no_grad():
+            r0 = renderer.render(batch)
+    finally:
+        torch.sort = orig_sort
+    out["render0_z_vals_f"] = sorted_z.pop().numpy()
     for k, v in r0.items():
         out["render0_" + k] = v.numpy()
     t_rand = torch.rand(64, 64, generator=g1)
@@ -150,12 +163,15 @@ def main():
 
     cfg.task_arg.perturb = 1
     torch.rand = fake_rand
+    torch.sort = spy_sort
     try:
         with torch.no_grad():
             r1 = renderer.render(batch)
     finally:
         torch.rand = orig_rand
+        torch.sort = orig_sort
         cfg.task_arg.perturb = 0
+    out["render1_z_vals_f"] = sorted_z.pop().numpy()
     out["render1_t_rand"], out["render1_u"] = t_rand.numpy(), u_imp.numpy()
     for k, v in r1.items():
         out["render1_" + k] = v.numpy()

@@ -185,6 +185,15 @@ def test_mlp_forward_large_and_density(cuda, ops, O, packers, seeded_state, dtyp
     assert float(dens[:, :3].abs().max()) == 0.0
 
 
+def _oracle_mlp_grads(O, seeded_state, pts, vd, gout, spd, dt):
+    M = pts.shape[0]
+    dirs = vd[:, None].expand(-1, spd, 3).reshape(M, 3)
+    emb = torch.cat([O.positional_encoding(pts, 10), O.positional_encoding(dirs, 4)], -1).to(dt)
+    prm = {k: v.to(dt).clone().requires_grad_(True) for k, v in seeded_state.items() if k.startswith("model.")}
+    (O.mlp(O.split_params(prm, "model"), emb[:, :63], emb[:, 63:]) * gout.to(dt)).sum().backward()
+    return {k[len("model."):]: v.grad.double() for k, v in prm.items()}
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_mlp_backward(cuda, ops, O, seeded_state, dtype):
     g = torch.Generator().manual_seed(12)
@@ -192,17 +201,14 @@ def test_mlp_backward(cuda, ops, O, seeded_state, dtype):
     pts = torch.rand(M, 3, generator=g) * 3 - 1.5
     vd = torch.nn.functional.normalize(torch.randn(100, 3, generator=g), dim=-1)
     gout = torch.randn(M, 4, generator=g)
-    ref_params = {k: v.clone().requires_grad_(True) for k, v in seeded_state.items() if k.startswith("model.")}
-    p = O.split_params(ref_params, "model")
-    ref = O.network_forward(p, pts.reshape(100, 10, 3), vd).reshape(M, 4)
-    (ref * gout).sum().backward()
+    ref = _oracle_mlp_grads(O, seeded_state, pts, vd, gout, 10, torch.float32)
     params = [seeded_state[f"model.{n}"].to(cuda).clone().requires_grad_(True) for n in ops.NET_PARAM_NAMES]
     packer = ops.PackedMLP(params)
     raw = ops.mlp(packer, pts.to(cuda), vd.to(cuda), 10, dtype=dtype)
     (raw * gout.to(cuda)).sum().backward()
     for name, prm in zip(ops.NET_PARAM_NAMES, params):
-        r = ref_params[f"model.{name}"].grad
-        gg = prm.grad.cpu()
+        r = ref[name]
+        gg = prm.grad.cpu().double()
         if dtype == "fp32":
             err = float((gg - r).abs().max()) / (float(r.abs().max()) + 1e-12)
             assert err < 1e-4, (name, err)
@@ -212,6 +218,80 @@ def test_mlp_backward(cuda, ops, O, seeded_state, dtype):
             rel = float((gg - r).norm() / (r.norm() + 1e-12))
             cos = float(torch.nn.functional.cosine_similarity(gg.reshape(1, -1), r.reshape(1, -1)))
             assert rel < 0.2 and cos > 0.98, (name, rel, cos)
+
+
+def _decode_masks(masks_u8, M):
+    """[nblk, 68, 64] uint16 ReLU masks (bit rho of lane l = sample 32 blk + (l & 31),
+    feature acc_row(rho, l >> 5) of the tile) -> {tile: bool [M, 32]}."""
+    m = masks_u8.view(torch.int16).cpu().numpy().view(np.uint16).reshape(-1, 68, 64)
+    bits = (m[..., None] >> np.arange(16, dtype=np.uint16)) & 1  # [nblk, 68, 64, 16]
+    out = np.zeros((m.shape[0], 68, 32, 32), dtype=bool)  # [blk, tile, sample, feature]
+    for lane in range(64):
+        for rho in range(16):
+            out[:, :, lane & 31, (rho & 3) + 8 * (rho >> 2) + 4 * (lane >> 5)] = bits[:, :, lane, rho]
+    out = out.transpose(1, 0, 2, 3).reshape(68, -1, 32)[:, :M]
+    return torch.from_numpy(out)
+
+
+def _masked_mlp(p, x63, d27, mk):
+    """oracle.mlp with each ReLU replaced by the kernel's own mask (identical branch choices)."""
+    F = torch.nn.functional
+    hmask = lambda tile0, n: torch.cat([mk[tile0 + j] for j in range(n)], 1).to(x63.dtype)  # noqa: E731
+    h = x63
+    for i in range(8):
+        h = F.linear(h, *p[f"pts_linears.{i}"]) * hmask(8 * i, 8)
+        if i == 4:
+            h = torch.cat([x63, h], -1)
+    alpha = F.linear(h, *p["alpha_linear"])
+    feat = F.linear(h, *p["feature_linear"])
+    hv = F.linear(torch.cat([feat, d27], -1), *p["views_linears.0"]) * hmask(64, 4)
+    return torch.cat([F.linear(hv, *p["rgb_linear"]), alpha], -1)
+
+
+@pytest.mark.parametrize("dtype,M", [("fp32", 20010), ("bf16", 20010), ("bf16", 131101)])
+def test_mlp_backward_kernel_masks(cuda, ops, O, seeded_state, dtype, M):
+    """Many dW sample chunks (the last partial) and a ragged final block, against an fp64
+    oracle that takes the kernel's own ReLU masks: at these sizes a few pre-activations sit
+    within fp32 rounding of 0, and any two fp32 evaluations (the oracle's own fp32 vs fp64
+    included) pick different branches there -- forcing the branches isolates the GEMMs.
+    fp32: 1e-4 of the largest entry; bf16 (operands rounded to 8 bits): 2e-2 in norm."""
+    from nerf_amd._lib import lib, ptr, stream_of
+    g = torch.Generator().manual_seed(12)
+    spd = 10
+    pts = torch.rand(M, 3, generator=g) * 3 - 1.5
+    vd = torch.nn.functional.normalize(torch.randn(-(-M // spd), 3, generator=g), dim=-1)
+    gout = torch.randn(M, 4, generator=g)
+    params = [seeded_state[f"model.{n}"].to(cuda).clone().requires_grad_(True) for n in ops.NET_PARAM_NAMES]
+    packer = ops.PackedMLP(params)
+    code = ops.dtype_code(dtype)
+    # the kernel's masks: the same forward, with its training stores into our own buffers
+    pc, vc = pts.to(cuda), vd.to(cuda)
+    act = torch.empty(lib().nerf_mlp_act_bytes(code, M), dtype=torch.uint8, device=cuda)
+    masks = torch.empty(lib().nerf_mlp_mask_bytes(M), dtype=torch.uint8, device=cuda)
+    raw0 = torch.empty(M, 4, device=cuda)
+    assert lib().nerf_mlp_fwd(ptr(packer.get(code, 0)), code, ptr(pc), ptr(vc), spd, None, M, 1, ptr(raw0), ptr(act),
+                              ptr(masks), stream_of(pc)) == 0
+    raw = ops.mlp(packer, pc, vc, spd, dtype=dtype)
+    (raw * gout.to(cuda)).sum().backward()
+    torch.testing.assert_close(raw0, raw.detach(), rtol=0, atol=0)  # deterministic forward
+    mk = _decode_masks(masks, M)
+
+    dirs = vd[:, None].expand(-1, spd, 3).reshape(-1, 3)[:M]
+    emb = torch.cat([O.positional_encoding(pts, 10), O.positional_encoding(dirs, 4)], -1).double()
+    prm = {k: v.double().clone().requires_grad_(True) for k, v in seeded_state.items() if k.startswith("model.")}
+    ref = _masked_mlp(O.split_params(prm, "model"), emb[:, :63], emb[:, 63:], mk)
+    (ref * gout.double()).sum().backward()
+    if dtype == "fp32":
+        np.testing.assert_allclose(raw.detach().cpu().double().numpy(), ref.detach().numpy(), rtol=0, atol=1e-4)
+    for name, prm_g in zip(ops.NET_PARAM_NAMES, params):
+        r = prm[f"model.{name}"].grad
+        gg = prm_g.grad.cpu().double()
+        if dtype == "fp32":
+            err = float((gg - r).abs().max()) / (float(r.abs().max()) + 1e-30)
+            assert err < 1e-4, (name, err)
+        else:
+            rel = float((gg - r).norm() / (r.norm() + 1e-30))
+            assert rel < 2e-2, (name, rel)
 
 
 # ---------------------------------------------------------------------------------- grid

@@ -35,6 +35,15 @@ def _batch(golden, cuda, n=64):
 
 KEYS = ["rgb_map_c", "depth_map_c", "acc_map_c", "rgb_map_f", "depth_map_f", "acc_map_f"]
 
+# End to end, the fine pass sees the CDF of the coarse weights.  With the seed-0 (untrained)
+# net the coarse weights are ~1e-3 and alpha = 1 - exp(-sigma*delta) carries an absolute
+# rounding error of ~1 ulp(1.0) on either side (CPU vs GPU exp, MKL vs MFMA accumulation
+# order), i.e. ~1e-4 relative: CDF entries move by ~1e-5, a few importance samples move to
+# the neighbouring bin, and the fine depth (range 2..6) moves by up to ~3e-4.  Given the
+# *same* CDF (north_star: indices bit-exact for identical CDF inputs) the fine pass is held to
+# 1e-4 below (test_fine_pass_given_reference_samples).
+E2E_FINE_DEPTH_TOL = 6e-4
+
 
 @pytest.mark.parametrize("dtype,tol", [("fp32", 1e-4), ("bf16", 2e-3)])
 def test_render_perturb0(golden, cuda, stack, dtype, tol):
@@ -46,8 +55,29 @@ def test_render_perturb0(golden, cuda, stack, dtype, tol):
     for k in KEYS:
         ref = golden[f"render0_{k}"]
         t = tol * (6.0 if "depth" in k else 1.0) if dtype == "bf16" else tol
+        if k == "depth_map_f" and dtype == "fp32":
+            t = E2E_FINE_DEPTH_TOL
         np.testing.assert_allclose(out[k].cpu().numpy(), ref, rtol=0, atol=t, err_msg=k)
     net.mlp_dtype = "fp32"
+
+
+@pytest.mark.parametrize("perturb", [False, True])
+def test_fine_pass_given_reference_samples(golden, cuda, stack, perturb):
+    """Fine MLP + compositing on the reference's own merged depths (captured from its
+    torch.sort in make_golden.py): rgb/depth/acc within 1e-4 of the reference's outputs."""
+    from nerf_amd import ops
+    cfg, net, r = stack
+    tag = "render1" if perturb else "render0"
+    rc = torch.from_numpy(golden["rays"][:64]).to(cuda)
+    zf = torch.from_numpy(golden[f"{tag}_z_vals_f"]).to(cuda)
+    with torch.no_grad():
+        pts = rc[:, None, :3] + rc[:, None, 3:] * zf[..., None]
+        vd = rc[:, 3:] / torch.norm(rc[:, 3:], dim=-1, keepdim=True)
+        raw_f = net(pts, vd, "fine")
+        rgb, dep, acc, _ = ops.composite(raw_f, zf, rc[:, 3:6], True)
+    np.testing.assert_allclose(rgb.cpu().numpy(), golden[f"{tag}_rgb_map_f"], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(dep.cpu().numpy(), golden[f"{tag}_depth_map_f"], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(acc.cpu().numpy(), golden[f"{tag}_acc_map_f"], rtol=0, atol=1e-4)
 
 
 def test_render_perturb1_injected(golden, cuda, stack, O=None):
@@ -67,7 +97,8 @@ def test_render_perturb1_injected(golden, cuda, stack, O=None):
     got = dict(rgb_map_c=rgb_c, depth_map_c=dep_c, acc_map_c=acc_c, rgb_map_f=rgb_f, depth_map_f=dep_f,
                acc_map_f=acc_f)
     for k in KEYS:
-        np.testing.assert_allclose(got[k].cpu().numpy(), golden[f"render1_{k}"], rtol=0, atol=1e-4, err_msg=k)
+        t = E2E_FINE_DEPTH_TOL if k == "depth_map_f" else 1e-4
+        np.testing.assert_allclose(got[k].cpu().numpy(), golden[f"render1_{k}"], rtol=0, atol=t, err_msg=k)
 
 
 def test_loss_gradients_match_reference(golden, cuda, stack):

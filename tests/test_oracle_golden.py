@@ -76,13 +76,12 @@ def test_render_both_modes(golden, seeded_state):
     rays = T(golden, "rays")[:64]
     near, far = torch.tensor([2.0]), torch.tensor([6.0])
     with torch.no_grad():
-        r0 = O.render(C, F, rays, near, far)
+        r0 = O.render(C, F, rays, near, far, keep=True)
         r1 = O.render(C, F, rays, near, far, perturb=True, t_rand=T(golden, "render1_t_rand"),
-                      u=T(golden, "render1_u"))
-    for k, v in r0.items():
-        np.testing.assert_array_equal(v.numpy(), golden["render0_" + k])
-    for k, v in r1.items():
-        np.testing.assert_array_equal(v.numpy(), golden["render1_" + k])
+                      u=T(golden, "render1_u"), keep=True)
+    for tag, r in (("render0_", r0), ("render1_", r1)):
+        for k in ("rgb_map_c", "depth_map_c", "acc_map_c", "rgb_map_f", "depth_map_f", "acc_map_f", "z_vals_f"):
+            np.testing.assert_array_equal(r[k].numpy(), golden[tag + k], err_msg=tag + k)
 
 
 def test_gradients(golden, seeded_state):
