@@ -91,7 +91,9 @@ int nerf_composite_bwd(const float* raw, const float* z, const float* dirs, int 
  * optimizer step); dir 0 = forward, 1 = backward (W^T).
  * fwd: raw [M,4] = (rgb logits, sigma pre-activation) for pts [M,3]; view direction of
  * sample m is viewdirs[dir_index ? dir_index[m] : m / samples_per_dir].
- * bwd: accumulates into grad[nerf_mlp_net_params()] (flat, state_dict order). */
+ * bwd: accumulates into grad[nerf_mlp_net_params()] (flat, state_dict order).
+ * act / masks / dz are opaque workspaces of nerf_mlp_{act,mask,dz}_bytes(M) bytes written by the
+ * training forward (flags & NERF_MLP_STORE) and the dX chain; their layouts are internal. */
 int64_t nerf_mlp_net_params(void);
 int64_t nerf_mlp_param_offset(int i);
 int64_t nerf_mlp_packed_bytes(int dtype, int dir);

@@ -20,6 +20,8 @@
 #include "common.h"
 #include "mlp_tables.h"
 
+#include <utility>
+
 namespace nerf {
 namespace mlp {
 
@@ -35,6 +37,7 @@ struct PF32 {
   static constexpr int WAVES = 4;  // one wave per SIMD (<= 512 VGPR+AGPR)
   static constexpr int ESIZE = 4;
   static constexpr int SPL = 4;    // samples per 16-B lane load (dW GEMM)
+  static constexpr bool FAST_PE = false;  // fp32 parity path: libm-accurate sincosf
   using Store = float;
   struct Tile { float v[16]; };
   static __device__ __forceinline__ f32x16 mma(uint4 a, const Tile& b, int c, f32x16 acc) {
@@ -69,6 +72,7 @@ struct PBF16 {
   static constexpr int WAVES = 8;  // two waves per SIMD (<= 256 VGPR)
   static constexpr int ESIZE = 2;
   static constexpr int SPL = 8;
+  static constexpr bool FAST_PE = true;   // PE rounded to bf16 anyway: v_sin_f32 after f64 reduction
   using Store = __bf16;
   struct Tile { bf16x8 b[2]; };
   static __device__ __forceinline__ f32x16 mma(uint4 a, const Tile& b, int c, f32x16 acc) {
@@ -109,9 +113,21 @@ __host__ __device__ constexpr int64_t total_chunks(int ch, int dir) {
 
 struct ParamPtrs { const float* p[NPARAM]; };
 
+// first chunk of every unit (+ the end), evaluated at compile time and passed by value:
+// the unit of a chunk is then a scan of kernel arguments, not a runtime walk of the
+// constexpr layout functions (which are loops)
+struct UnitOffsets { int off[NUNIT_FWD + 1]; };
+template <int CH, int DIR>
+constexpr UnitOffsets unit_offsets() {
+  UnitOffsets t{};
+  const int nu = DIR == 0 ? NUNIT_FWD : NUNIT_BWD;
+  for (int u = 0; u <= nu; ++u) t.off[u] = DIR == 0 ? fwd_unit_chunk_off(u, CH) : bwd_unit_chunk_off(u, CH);
+  return t;
+}
+
 // one thread per 16-B lane slot of one chunk
 template <class P, int DIR>
-__global__ void pack_kernel(ParamPtrs prm, char* out) {
+__global__ void pack_kernel(ParamPtrs prm, UnitOffsets uo, char* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total_chunks(P::CH, DIR) * 64) return;
   const int lane = (int)(i & 63);
@@ -119,10 +135,8 @@ __global__ void pack_kernel(ParamPtrs prm, char* out) {
   const int r = lane & 31, h = lane >> 5;
   const int nunit = DIR == 0 ? NUNIT_FWD : NUNIT_BWD;
   int u = 0;
-  while (u + 1 < nunit &&
-         (DIR == 0 ? fwd_unit_chunk_off(u + 1, P::CH) : bwd_unit_chunk_off(u + 1, P::CH)) <= chunk)
-    ++u;
-  const int within = chunk - (DIR == 0 ? fwd_unit_chunk_off(u, P::CH) : bwd_unit_chunk_off(u, P::CH));
+  for (int k = 1; k < nunit; ++k) u += uo.off[k] <= chunk ? 1 : 0;
+  const int within = chunk - uo.off[u];
   char* dst = out + i * 16;
   if (DIR == 0 && within == fwd_unit_tiles(u) * P::CH) {
     // bias chunk: lanes 0..7 hold the 32 biases of the unit's output rows, rest zero
@@ -161,43 +175,138 @@ __global__ void pack_kernel(ParamPtrs prm, char* out) {
 }
 
 // ------------------------------------------------------------------------------------
-// weight stream: 2-slot LDS ring filled by global_load_lds (1 KiB per wave-instruction)
+// weight stream.  The packed units (one 32-row output tile of one layer, forward; one
+// 32-row output tile of one dX stage, backward) are cut into GROUPS of consecutive units
+// of one layer/stage that fit one LDS slot (<= SLOT_CAP KiB).  A 2-slot ring is filled by
+// LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction) one group ahead, so a
+// workgroup meets one barrier per group (4 hidden-layer units = 64 MFMAs per wave in
+// bf16) instead of one per unit.
+//
+// The DMA is issued from inline asm, invisible to hipcc's waitcnt bookkeeping, and the
+// group hand-off is a counted `s_waitcnt vmcnt(N)` + s_barrier where N = the vector-memory
+// instructions this wave issued after the next group's DMA (the group's activation /
+// gradient stores).  Loads, stores and LDS-DMA retire in issue order on one counter
+// (MI355X_MICROARCH.md), so the wait covers the DMA and never the stores.  No
+// compiler-visible global load may sit between a DMA and its wait (its compiler wait
+// would drain the ring): all such loads are in the prologue.
 // ------------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void lds_void;
 
-__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)lds_wave_base, 16, 0, 0);
-}
-
-// The same LDS-DMA hidden from hipcc's waitcnt bookkeeping: hipcc waits vmcnt(0) before
-// any ds_read_tr while one of its own LDS-DMAs is pending, which would drain a multi-block
-// ring.  The caller owns completion (counted s_waitcnt vmcnt + s_barrier before reading).
 __device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t lds_wave_base) {
   uint32_t saved;  // m0 is reserved to the compiler: save and restore it around the DMA
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(saved) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_wave_base)) : "memory");
 }
 
-template <class P, int SLOT_CHUNKS>
-struct Stream {
-  const uint4* g;  // chunk c of the packed buffer starts at g + 64 c
-  uint4* lds;
-  int slot;
-  // issue the copy of `n` chunks starting at global chunk `c0` into slot `to`
-  __device__ __forceinline__ void fetch(int c0, int n, int to) const {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int k = wave; k < n; k += P::WAVES)
-      glds16(g + (int64_t)(c0 + k) * 64 + lane, lds + (to * SLOT_CHUNKS + k) * 64);
+// every younger-than-N vector memory op of this wave may still be in flight; all LDS ops
+// done; then the workgroup barrier.  "memory": no LDS/global access crosses it.
+template <int N>
+__device__ __forceinline__ void wait_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// hand a loaded value to an empty asm right after a prologue wait: hipcc then places its
+// own wait for the load there (already satisfied) instead of at the first use in the main
+// loop, where it would also drain the in-flight weight DMA
+__device__ __forceinline__ void settle(float& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void settle(uint32_t& x) { asm volatile("" : "+v"(x)); }
+
+template <int... I, class F>
+__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+// compile-time unrolled loop: f(std::integral_constant<int, i>) for i in [0, N)
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+__host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
+
+constexpr int SLOT_CAP = 72;   // KiB (1 KiB chunks) per ring slot: 2 x 72 KiB of 160 KiB LDS
+constexpr int NSLOT = 2;
+constexpr int GROUP_MAX = 8;   // units per group
+
+struct Group { int u0, n, c0, nch; };  // first unit, units, first chunk, chunks
+
+// DIR 0: forward units (DENSITY: trunk + alpha only, occupancy_grid.py:60 reads raw[...,3]);
+// DIR 1: dX-chain units
+template <int DIR, bool DENSITY>
+__host__ __device__ constexpr bool unit_used(int u) {
+  return DIR != 0 || !DENSITY || u < fwd_unit_first(LFA) || u == fwd_unit_first(LFA) + 8;
+}
+template <int DIR> __host__ __device__ constexpr int unit_seg(int u) {
+  return DIR == 0 ? fwd_unit_layer(u) : bwd_unit_stage(u);
+}
+template <int DIR> __host__ __device__ constexpr int unit_chunks(int u, int ch) {
+  return DIR == 0 ? fwd_unit_chunks(u, ch) : bwd_unit_chunks(u, ch);
+}
+template <int DIR> __host__ __device__ constexpr int unit_chunk_off(int u, int ch) {
+  return DIR == 0 ? fwd_unit_chunk_off(u, ch) : bwd_unit_chunk_off(u, ch);
+}
+
+// greedy grouping: consecutive used units of one segment while the slot has room
+template <int DIR, bool DENSITY, int CH>
+struct Groups {
+  Group g[NUNIT_FWD > NUNIT_BWD ? NUNIT_FWD : NUNIT_BWD];
+  int n;
+  __host__ __device__ constexpr Groups() : g(), n(0) {
+    const int NU = DIR == 0 ? NUNIT_FWD : NUNIT_BWD;
+    int u = 0;
+    while (u < NU) {
+      if (!unit_used<DIR, DENSITY>(u)) {
+        ++u;
+        continue;
+      }
+      Group G{u, 0, unit_chunk_off<DIR>(u, CH), 0};
+      const int seg = unit_seg<DIR>(u);
+      while (u < NU && unit_used<DIR, DENSITY>(u) && unit_seg<DIR>(u) == seg && G.n < GROUP_MAX &&
+             G.nch + unit_chunks<DIR>(u, CH) <= SLOT_CAP) {
+        G.nch += unit_chunks<DIR>(u, CH);
+        ++G.n;
+        ++u;
+      }
+      g[n++] = G;
+    }
   }
-  __device__ __forceinline__ const uint4* cur() const { return lds + slot * SLOT_CHUNKS * 64; }
+};
+template <int DIR, bool DENSITY, int CH>
+struct GroupTable {
+  static constexpr Groups<DIR, DENSITY, CH> t{};
 };
 
+// issue the DMA of group G into slot `slot`: every wave issues exactly NF wave-instructions
+// (the last chunk is re-copied by the surplus waves -- identical bytes), so the count a
+// later wait needs is a compile-time constant.
+template <class P, int C0, int NCH>
+__device__ __forceinline__ void fetch_group(const uint4* gsrc, uint32_t slot_base, int wave, int lane) {
+  constexpr int NF = (NCH + P::WAVES - 1) / P::WAVES;
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int k = cmin(wave + P::WAVES * i, NCH - 1);
+    glds16_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
+  }
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const u32x4 lds_cu4;
+__device__ __forceinline__ uint4 as_uint4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+
+// per-lane LDS base of a unit's chunks (lane-linear: + 16 lane bytes), laundered through
+// an empty asm: every read of the unit is then this one VGPR + an immediate offset
+// (< 64 KiB).  Left visible, hipcc materialises one address VGPR per distinct chunk offset
+// of both ring slots and keeps them all live across the unrolled kernel.
+__device__ __forceinline__ lds_cu4* lds_ptr(uint32_t byte_addr) {
+  settle(byte_addr);
+  return (lds_cu4*)(uintptr_t)byte_addr;
+}
+
 template <class P>
-__device__ __forceinline__ f32x16 tile_mma(const uint4* slot_base, int tile_idx, const typename P::Tile& b,
-                                           f32x16 acc, int lane) {
+__device__ __forceinline__ f32x16 tile_mma(lds_cu4* unit_lane, int tile_idx, const typename P::Tile& b, f32x16 acc) {
 #pragma unroll
   for (int c = 0; c < P::CH; ++c) {
-    uint4 a = slot_base[(tile_idx * P::CH + c) * 64 + lane];
+    const uint4 a = as_uint4(unit_lane[(tile_idx * P::CH + c) * 64]);
     acc = P::mma(a, b, c, acc);
   }
   return acc;
@@ -207,25 +316,64 @@ __device__ __forceinline__ f32x16 tile_mma(const uint4* slot_base, int tile_idx,
 // positional encoding straight into accumulator-layout tiles
 // (freq.py:7-32: [x, sin(2^k x), cos(2^k x)]_k; feature 3 + 6k + {0..2 sin, 3..5 cos})
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ float pe_feature(int f, int nfreq, float x0, float x1, float x2) {
-  if (f < 3) return f == 0 ? x0 : f == 1 ? x1 : x2;
-  const int g = f - 3;
-  const int k = g / 6, r = g - 6 * k;
-  if (k >= nfreq) return 0.f;
-  const int dim = r % 3;
-  const float x = dim == 0 ? x0 : dim == 1 ? x1 : x2;
-  const float a = x * (float)(1 << k);  // exact power-of-two scale, as x * 2.**k in torch
-  return r < 3 ? sinf(a) : cosf(a);
+// feature f of an nfreq-band encoding -> (kind, coordinate, band, cos?)
+//   kind 0: zero (padding), 1: the raw coordinate, 2: sin/cos(x_dim * 2^k)
+struct PeFeat { int kind, dim, k, cos; };
+__host__ __device__ constexpr PeFeat pe_feat(int f, int nfreq, int nvalid) {
+  if (f >= nvalid) return PeFeat{0, 0, 0, 0};
+  if (f < 3) return PeFeat{1, f, 0, 0};
+  const int g = f - 3, k = g / 6, r = g % 6;
+  if (k >= nfreq) return PeFeat{0, 0, 0, 0};
+  return PeFeat{2, r % 3, k, r >= 3 ? 1 : 0};
 }
 
-template <class P>
-__device__ __forceinline__ void pe_tile(typename P::Tile& t, int tile, int nfreq, int nvalid, int h, float x0,
-                                        float x1, float x2) {
-#pragma unroll
-  for (int rho = 0; rho < 16; ++rho) {
-    const int f = 32 * tile + acc_row(rho, h);
-    P::set(t, rho, f < nvalid ? pe_feature(f, nfreq, x0, x1, x2) : 0.f);
+// sin or cos of x * 2^k.  FAST: the angle in revolutions, x * (2^k / 2pi) + (cos ? 1/4 : 0),
+// reduced exactly enough in f64 (|x 2^k| < 2^13 rad keeps ~40 fractional bits), then
+// v_sin_f32 on [0,1) revolutions -- far inside bf16 resolution.  Accurate: one libm
+// sincosf of the exact fp32 product x * 2^k (as torch computes x * 2.**k, then sin/cos).
+template <bool FAST>
+__device__ __forceinline__ float pe_trig(float x, double scale_rev, float scale_rad, double phase, bool is_cos) {
+  if constexpr (FAST) {
+    const double t = __builtin_fma((double)x, scale_rev, phase);
+    return __builtin_amdgcn_sinf((float)(t - __builtin_floor(t)));
+  } else {
+    float s, c;
+    sincosf(x * scale_rad, &s, &c);
+    return is_cos ? c : s;
   }
+}
+
+// positional encoding straight into accumulator-layout tiles (freq.py:7-32:
+// [x, sin(2^k x), cos(2^k x)]_k, feature 3 + 6k + {0..2 sin, 3..5 cos}).  Register rho of
+// lane l holds feature 32 tile + acc_row(rho, l >> 5): the two lane halves differ by 4
+// features, so each register selects between two compile-time feature descriptors.
+template <class P, int TILE, int NFREQ, int NVALID>
+__device__ __forceinline__ void pe_tile(typename P::Tile& t, int h, float x0, float x1, float x2) {
+  constexpr double INV2PI = 0.15915494309189533576888376337251;
+  sfor<16>([&](auto rr) {
+    constexpr int rho = decltype(rr)::value;
+    constexpr PeFeat A = pe_feat(32 * TILE + acc_row(rho, 0), NFREQ, NVALID);
+    constexpr PeFeat B = pe_feat(32 * TILE + acc_row(rho, 1), NFREQ, NVALID);
+    float v;
+    if constexpr (A.kind == 0 && B.kind == 0) {
+      v = 0.f;
+    } else {
+      const int dim = h ? B.dim : A.dim;
+      const float x = dim == 0 ? x0 : dim == 1 ? x1 : x2;
+      float trig = 0.f;
+      if constexpr (A.kind == 2 || B.kind == 2) {
+        constexpr int ka = A.kind == 2 ? A.k : (B.kind == 2 ? B.k : 0);
+        constexpr int kb = B.kind == 2 ? B.k : ka;
+        const int k = h ? kb : ka;
+        const bool is_cos = h ? (B.cos != 0) : (A.cos != 0);
+        const double srev = INV2PI * (double)(1 << k);
+        trig = pe_trig<P::FAST_PE>(x, srev, (float)(1 << k), is_cos ? 0.25 : 0.0, is_cos);
+      }
+      const int kind = h ? B.kind : A.kind;
+      v = kind == 2 ? trig : kind == 1 ? x : 0.f;
+    }
+    P::set(t, rho, v);
+  });
 }
 
 // fragment-native store of one finished tile (mlp_tables.h, "Training stores"): CH
@@ -238,6 +386,33 @@ __device__ __forceinline__ void store_tile(void* base, int64_t nblk, int tau, in
   for (int c = 0; c < P::CH; ++c) dst[c * 64] = P::chunk(t, c);
 }
 
+// bias chunk of a unit: lanes 0..7 hold its 32 fp32 biases; rows 8q + 4h + {0..3} =
+// lane (2q + h).  `half` points at lane h of the chunk.
+__device__ __forceinline__ f32x16 bias_init(lds_cu4* half) {
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint4 b = as_uint4(half[2 * q]);
+    acc[4 * q + 0] = __uint_as_float(b.x);
+    acc[4 * q + 1] = __uint_as_float(b.y);
+    acc[4 * q + 2] = __uint_as_float(b.z);
+    acc[4 * q + 3] = __uint_as_float(b.w);
+  }
+  return acc;
+}
+
+// ReLU masks of the training forward, read by the dX chain: per 32-sample wave block,
+// MASK_GROUPS x 64 lanes x 16 B; group l < 8 = layer l's 8 output tiles (tile n -> dword
+// n >> 1, bits 16 (n & 1) + rho), group 8 = the view layer's 4 tiles.  One 16-byte store
+// per lane per layer.
+__device__ __forceinline__ uint4* mask_slot(void* masks, int64_t wblock, int grp, int lane) {
+  return (uint4*)masks + (wblock * MASK_GROUPS + grp) * 64 + lane;
+}
+
+// ------------------------------------------------------------------------------------
+// forward: one wave = 32 samples through all 11 layers; activations stay in registers
+// (feature-major accumulator layout = the next layer's B operand).
+// ------------------------------------------------------------------------------------
 struct FwdArgs {
   const char* wpack;
   const float* pts;          // [M,3]
@@ -248,295 +423,312 @@ struct FwdArgs {
   int64_t nblk;              // 32-sample blocks of the stores (M padded to M_ALIGN) / 32
   float* raw;                // [M,4]
   void* act;                 // [AT_TILES][nblk] tile-blocks or null
-  uint16_t* masks;           // [nblk, MASK_TILES, 64] or null
+  void* masks;               // [nblk][MASK_GROUPS][64] x 16 B or null
 };
 
-// activation of a finished accumulator tile -> next layer's B operand (+ training stores)
-template <class P, bool RELU, bool STORE>
-__device__ __forceinline__ void finish_tile(const f32x16& acc, typename P::Tile& out, const FwdArgs& a, int act_tile,
-                                            int mask_tile, int64_t m, int64_t wblock, int h, int lane) {
-  uint32_t mask = 0;
+template <class P, bool STORE, bool DENSITY>
+struct FwdWave {
+  using Tile = typename P::Tile;
+  static constexpr int CH = P::CH;
+  using GT = GroupTable<0, DENSITY, P::CH>;
+
+  const FwdArgs& a;
+  const uint4* gw;
+  const uint4* lds;
+  uint32_t lds_base;
+  int lane, wave, h;
+  int64_t wblock, m;
+  float px, py, pz, dx, dy, dz;
+  Tile X[2], D, Ha[8], Hb[8];
+  uint32_t mw[4];
+  float alpha, rgb0, rgb1, rgb2;
+
+  __device__ __forceinline__ FwdWave(const FwdArgs& args, const uint4* smem) : a(args), lds(smem) {
+    gw = (const uint4*)a.wpack;
+    lds_base = (uint32_t)(uintptr_t)(lds_void*)smem;
+    lane = threadIdx.x & 63;
+    wave = threadIdx.x >> 6;
+    h = lane >> 5;
+    wblock = (int64_t)blockIdx.x * P::WAVES + wave;
+    m = wblock * 32 + (lane & 31);
+  }
+
+  template <int g> __device__ __forceinline__ void fetch() {
+    constexpr Group G = GT::t.g[g];
+    fetch_group<P, G.c0, G.nch>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
+  }
+
+  // input tile t of layer L (mlp_tables.h: Ha/Hb ping-pong, PE tiles X / D)
+  template <int L, int t> __device__ __forceinline__ const Tile& in_tile() const {
+    if constexpr (L == L0) return X[t];
+    else if constexpr (L == L5) { if constexpr (t < 2) return X[t]; else return Ha[t - 2]; }
+    else if constexpr (L == LV) { if constexpr (t < 8) return Ha[t]; else return D; }
+    else if constexpr (L == LRGB) return Hb[t];
+    else if constexpr (L == L1 || L == L3 || L == L7) return Ha[t];
+    else return Hb[t];  // L2, L4, L6, LFA
+  }
+  template <int L> __device__ __forceinline__ Tile* out_arr() {
+    if constexpr (L == L0 || L == L2 || L == L4 || L == L6 || L == LFA) return Ha;
+    else return Hb;  // L1, L3, L5, L7, LV
+  }
+
+  // vector-memory stores issued by unit u's finish
+  static __host__ __device__ constexpr int unit_stores(int u) {
+    if (!STORE) return 0;
+    const int L = fwd_unit_layer(u), n = u - fwd_unit_first(L);
+    if (L == LFA) return n < 8 ? CH : 0;
+    if (L == LRGB) return 0;
+    return CH + (n == fwd_out_tiles(L) - 1 ? 1 : 0);  // + the layer's mask store
+  }
+  static __host__ __device__ constexpr int group_stores(int g) {
+    int s = 0;
+    for (int j = 0; j < GT::t.g[g].n; ++j) s += unit_stores(GT::t.g[g].u0 + j);
+    return s;
+  }
+
+  template <int L, int n> __device__ __forceinline__ void finish(const f32x16& acc) {
+    if constexpr (L <= L7 || L == LV) {
+      Tile out;
+      uint32_t bits = 0;
 #pragma unroll
-  for (int rho = 0; rho < 16; ++rho) {
-    float x = acc[rho];
-    if (RELU) {
-      mask |= (x > 0.f ? 1u : 0u) << rho;
-      x = x > 0.f ? x : 0.f;
+      for (int rho = 0; rho < 16; ++rho) {
+        const float x = acc[rho];
+        bits |= (x > 0.f ? 1u : 0u) << rho;
+        P::set(out, rho, x > 0.f ? x : 0.f);
+      }
+      out_arr<L>()[n] = out;
+      if constexpr (STORE) {
+        store_tile<P>(a.act, a.nblk, (L == LV ? AT_V : AT_H + 8 * L) + n, wblock, lane, out);
+        if constexpr ((n & 1) == 0) mw[n >> 1] = bits;
+        else mw[n >> 1] |= bits << 16;
+        if constexpr (n == fwd_out_tiles(L) - 1)
+          *mask_slot(a.masks, wblock, L == LV ? 8 : L, lane) =
+              make_uint4(mw[0], mw[1], L == LV ? 0u : mw[2], L == LV ? 0u : mw[3]);
+      }
+    } else if constexpr (L == LFA) {
+      if constexpr (n < 8) {  // feature_linear: no activation
+        Tile out;
+#pragma unroll
+        for (int rho = 0; rho < 16; ++rho) P::set(out, rho, acc[rho]);
+        Ha[n] = out;
+        if constexpr (STORE) store_tile<P>(a.act, a.nblk, AT_F + n, wblock, lane, out);
+      } else {
+        alpha = acc[0];  // alpha_linear: output row 0 = register 0 of lanes 0..31
+      }
+    } else {  // LRGB: rows 0..2 = registers 0..2 of lanes 0..31
+      rgb0 = acc[0];
+      rgb1 = acc[1];
+      rgb2 = acc[2];
     }
-    P::set(out, rho, x);
   }
-  if (STORE) {
-    store_tile<P>(a.act, a.nblk, act_tile, wblock, lane, out);
-    if (RELU) a.masks[(wblock * MASK_TILES + mask_tile) * 64 + lane] = (uint16_t)mask;
+
+  template <int u> __device__ __forceinline__ void unit(uint32_t unit_addr) {
+    constexpr int L = fwd_unit_layer(u), n = u - fwd_unit_first(L);
+    constexpr int T = fwd_in_tiles(L);
+    if constexpr (L == L5 && n == 0) {  // PE recomputed for the skip instead of held through L1..L4
+      settle(px);  // opaque to hipcc: it would otherwise CSE this with the L0 tiles and hold them
+      settle(py);
+      settle(pz);
+      pe_tile<P, 0, 10, 63>(X[0], h, px, py, pz);
+      pe_tile<P, 1, 10, 63>(X[1], h, px, py, pz);
+    }
+    if constexpr (L == LV && n == 0) {
+      settle(dx);
+      settle(dy);
+      settle(dz);
+      pe_tile<P, 0, 4, 27>(D, h, dx, dy, dz);
+    }
+    f32x16 acc = bias_init(lds_ptr(unit_addr + (uint32_t)(T * CH * 1024 + h * 16)));
+    lds_cu4* w = lds_ptr(unit_addr + (uint32_t)(lane * 16));
+    sfor<T>([&](auto tt) {
+      constexpr int t = decltype(tt)::value;
+      acc = tile_mma<P>(w, t, in_tile<L, t>(), acc);
+    });
+    finish<L, n>(acc);
   }
-}
 
-__device__ __forceinline__ f32x16 bias_init(const uint4* bias_chunk, int h) {
-  f32x16 acc;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    // rows 8q + 4h + {0..3} = floats [8q+4h, 8q+4h+4) = lane (2q + h) of the bias chunk
-    uint4 b = bias_chunk[2 * q + h];
-    acc[4 * q + 0] = __uint_as_float(b.x);
-    acc[4 * q + 1] = __uint_as_float(b.y);
-    acc[4 * q + 2] = __uint_as_float(b.z);
-    acc[4 * q + 3] = __uint_as_float(b.w);
+  template <int g> __device__ __forceinline__ void step() {
+    constexpr Group G = GT::t.g[g];
+    constexpr int NG = GT::t.n;
+    if constexpr (g + 1 < NG) fetch<g + 1>();
+    sfor<G.n>([&](auto jj) {
+      constexpr int u = G.u0 + decltype(jj)::value;
+      unit<u>(lds_base + (uint32_t)(((g % NSLOT) * SLOT_CAP + unit_chunk_off<0>(u, CH) - G.c0) * 1024));
+      // one scheduling region per unit: hipcc would otherwise hoist every LDS read of the
+      // group (up to 256 VGPRs of A operands) to its top and spill
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if constexpr (g + 1 < NG) wait_barrier<group_stores(g)>();
   }
-  return acc;
-}
 
-template <class P> __host__ __device__ constexpr int fwd_slot_chunks() { return 10 * P::CH + 1; }
-template <class P> __host__ __device__ constexpr int dx_slot_chunks() { return 9 * P::CH; }
+  __device__ __forceinline__ void run() {
+    const int64_t ms = m < a.M ? m : a.M - 1;
+    px = a.pts[ms * 3 + 0];
+    py = a.pts[ms * 3 + 1];
+    pz = a.pts[ms * 3 + 2];
+    dx = dy = dz = 0.f;
+    if constexpr (!DENSITY) {
+      const int64_t di = a.dir_index ? (int64_t)a.dir_index[ms] : ms / a.samples_per_dir;
+      dx = a.dirs[di * 3 + 0];
+      dy = a.dirs[di * 3 + 1];
+      dz = a.dirs[di * 3 + 2];
+    }
+    fetch<0>();
+    pe_tile<P, 0, 10, 63>(X[0], h, px, py, pz);
+    pe_tile<P, 1, 10, 63>(X[1], h, px, py, pz);
+    if constexpr (STORE) {
+      Tile Dt;
+      pe_tile<P, 0, 4, 27>(Dt, h, dx, dy, dz);
+      store_tile<P>(a.act, a.nblk, AT_X, wblock, lane, X[0]);
+      store_tile<P>(a.act, a.nblk, AT_X + 1, wblock, lane, X[1]);
+      store_tile<P>(a.act, a.nblk, AT_D, wblock, lane, Dt);
+    }
+    wait_barrier<STORE ? 3 * CH : 0>();
+    settle(dx);
+    settle(dy);
+    settle(dz);
+    sfor<GT::t.n>([&](auto gg) { step<decltype(gg)::value>(); });
+    if (h == 0 && m < a.M)
+      *(float4*)(a.raw + m * 4) = DENSITY ? make_float4(0.f, 0.f, 0.f, alpha) : make_float4(rgb0, rgb1, rgb2, alpha);
+  }
+};
 
-// Forward.  Unit sequence = fwd_unit_*; the density-only variant (grid bake: only
-// raw[...,3] is used, occupancy_grid.py:60) jumps from the last trunk unit to alpha.
 template <class P, bool STORE, bool DENSITY>
 __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
-  using Tile = typename P::Tile;
-  constexpr int SC = fwd_slot_chunks<P>();
-  Stream<P, SC> ws{(const uint4*)a.wpack, smem_u4, 0};
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 5, c = lane & 31;
-  const int64_t wblock = (int64_t)blockIdx.x * P::WAVES + wave;
-  const int64_t m = wblock * 32 + c;
-  const int64_t ms = m < a.M ? m : a.M - 1;
-
-  constexpr int U_ALPHA = fwd_unit_first(LFA) + 8;
-  auto next_unit = [](int u) -> int {
-    if (DENSITY) {
-      if (u == fwd_unit_first(LFA) - 1) return U_ALPHA;
-      if (u == U_ALPHA) return -1;
-    }
-    return u + 1 < NUNIT_FWD ? u + 1 : -1;
-  };
-  f32x16 acc;
-  auto begin = [&](int u) {
-    const int nu = next_unit(u);
-    if (nu >= 0) ws.fetch(fwd_unit_chunk_off(nu, P::CH), fwd_unit_chunks(nu, P::CH), ws.slot ^ 1);
-    acc = bias_init(ws.cur() + fwd_unit_tiles(u) * P::CH * 64, h);
-  };
-  auto end = [&]() {
-    __syncthreads();  // vmcnt(0): next unit landed; everyone is done reading this slot
-    ws.slot ^= 1;
-  };
-
-  ws.fetch(fwd_unit_chunk_off(0, P::CH), fwd_unit_chunks(0, P::CH), 0);
-
-  const float px = a.pts[ms * 3 + 0], py = a.pts[ms * 3 + 1], pz = a.pts[ms * 3 + 2];
-  float dx = 0.f, dy = 0.f, dz = 0.f;
-  if (!DENSITY) {
-    const int64_t di = a.dir_index ? (int64_t)a.dir_index[ms] : ms / a.samples_per_dir;
-    dx = a.dirs[di * 3 + 0];
-    dy = a.dirs[di * 3 + 1];
-    dz = a.dirs[di * 3 + 2];
-  }
-  Tile Ha[8], Hb[8];
-  {
-    Tile X[2];
-    pe_tile<P>(X[0], 0, 10, 63, h, px, py, pz);
-    pe_tile<P>(X[1], 1, 10, 63, h, px, py, pz);
-    if (STORE) {
-      Tile D;
-      pe_tile<P>(D, 0, 4, 27, h, dx, dy, dz);
-      store_tile<P>(a.act, a.nblk, AT_X, wblock, lane, X[0]);
-      store_tile<P>(a.act, a.nblk, AT_X + 1, wblock, lane, X[1]);
-      store_tile<P>(a.act, a.nblk, AT_D, wblock, lane, D);
-    }
-    __syncthreads();
-    int unit = 0;
-    // ---- L0: PE(xyz) -> Ha
-#pragma unroll
-    for (int n = 0; n < 8; ++n, ++unit) {
-      begin(unit);
-      acc = tile_mma<P>(ws.cur(), 0, X[0], acc, lane);
-      acc = tile_mma<P>(ws.cur(), 1, X[1], acc, lane);
-      end();
-      finish_tile<P, true, STORE>(acc, Ha[n], a, AT_H + n, n, m, wblock, h, lane);
-    }
-  }
-  int unit = 8;
-  // ---- L1..L4 (ping-pong: L1 Ha->Hb, L2 Hb->Ha, L3 Ha->Hb, L4 Hb->Ha)
-#define NERF_HIDDEN_LAYER(L, IN, OUT)                                                            \
-  _Pragma("unroll") for (int n = 0; n < 8; ++n, ++unit) {                                        \
-    begin(unit);                                                                                 \
-    _Pragma("unroll") for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), t, IN[t], acc, lane); \
-    end();                                                                                       \
-    finish_tile<P, true, STORE>(acc, OUT[n], a, AT_H + (L) * 8 + n, (L) * 8 + n, m, wblock, h, lane);     \
-  }
-  NERF_HIDDEN_LAYER(1, Ha, Hb)
-  NERF_HIDDEN_LAYER(2, Hb, Ha)
-  NERF_HIDDEN_LAYER(3, Ha, Hb)
-  NERF_HIDDEN_LAYER(4, Hb, Ha)
-  // ---- L5: [PE(xyz), h4] -> Hb   (PE recomputed instead of held through L1..L4)
-  {
-    Tile X[2];
-    pe_tile<P>(X[0], 0, 10, 63, h, px, py, pz);
-    pe_tile<P>(X[1], 1, 10, 63, h, px, py, pz);
-#pragma unroll
-    for (int n = 0; n < 8; ++n, ++unit) {
-      begin(unit);
-      acc = tile_mma<P>(ws.cur(), 0, X[0], acc, lane);
-      acc = tile_mma<P>(ws.cur(), 1, X[1], acc, lane);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), 2 + t, Ha[t], acc, lane);
-      end();
-      finish_tile<P, true, STORE>(acc, Hb[n], a, AT_H + 5 * 8 + n, 5 * 8 + n, m, wblock, h, lane);
-    }
-  }
-  NERF_HIDDEN_LAYER(6, Hb, Ha)
-  NERF_HIDDEN_LAYER(7, Ha, Hb)
-#undef NERF_HIDDEN_LAYER
-  // ---- feature (no activation) -> Ha ; alpha (output row 0: lanes 0..31, register 0)
-  if (!DENSITY) {
-#pragma unroll
-    for (int n = 0; n < 8; ++n, ++unit) {
-      begin(unit);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), t, Hb[t], acc, lane);
-      end();
-      finish_tile<P, false, STORE>(acc, Ha[n], a, AT_F + n, 0, m, wblock, h, lane);
-    }
-  } else {
-    unit += 8;
-  }
-  float alpha;
-  {
-    begin(unit);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), t, Hb[t], acc, lane);
-    end();
-    alpha = acc[0];
-    ++unit;
-  }
-  if (DENSITY) {
-    if (h == 0 && m < a.M) *(float4*)(a.raw + m * 4) = make_float4(0.f, 0.f, 0.f, alpha);
-    return;
-  }
-  // ---- views: [feature, PE(dir)] -> Hb[0..3]
-  {
-    Tile D;
-    pe_tile<P>(D, 0, 4, 27, h, dx, dy, dz);
-#pragma unroll
-    for (int n = 0; n < 4; ++n, ++unit) {
-      begin(unit);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), t, Ha[t], acc, lane);
-      acc = tile_mma<P>(ws.cur(), 8, D, acc, lane);
-      end();
-      finish_tile<P, true, STORE>(acc, Hb[n], a, AT_V + n, 64 + n, m, wblock, h, lane);
-    }
-  }
-  // ---- rgb (rows 0..2: lanes 0..31, registers 0..2)
-  begin(unit);
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc = tile_mma<P>(ws.cur(), t, Hb[t], acc, lane);
-  end();
-  if (h == 0 && m < a.M) *(float4*)(a.raw + m * 4) = make_float4(acc[0], acc[1], acc[2], alpha);
+  FwdWave<P, STORE, DENSITY> w(a, smem_u4);
+  w.run();
 }
 
 // ------------------------------------------------------------------------------------
-// backward dX chain
+// backward dX chain: W^T products + ReLU masks, 32 samples per wave, storing every
+// layer's output gradient (pre-activation dZ) fragment-native for the dW GEMMs.
+// Stages (mlp_tables.h BStage): bRGB -> dZv, bV -> dfeature, bFA -> dZ7, b7..b1 -> dZ6..dZ0.
 // ------------------------------------------------------------------------------------
 struct DxArgs {
   const char* wpack_t;  // W^T chunks
   const float* d_raw;   // [M,4]
   int64_t M, nblk;
-  const uint16_t* masks;
+  const void* masks;    // [nblk][MASK_GROUPS][64] x 16 B
   void* dz;             // [ZT_TILES][nblk] tile-blocks
 };
 
-template <class P, bool MASK>
-__device__ __forceinline__ void dx_finish(const f32x16& acc, typename P::Tile& out, const DxArgs& a, int dz_tile,
-                                          int mask_tile, int64_t m, int64_t wblock, int h, int lane) {
-  const uint32_t mask = MASK ? (uint32_t)a.masks[(wblock * MASK_TILES + mask_tile) * 64 + lane] : 0xFFFFu;
+template <class P>
+struct DxWave {
+  using Tile = typename P::Tile;
+  static constexpr int CH = P::CH;
+  using GT = GroupTable<1, false, P::CH>;
+
+  const DxArgs& a;
+  const uint4* gw;
+  const uint4* lds;
+  uint32_t lds_base;
+  int lane, wave, h;
+  int64_t wblock, m;
+  Tile G, DA, Ha[8], Hb[8];
+  uint4 mk[MASK_GROUPS];
+
+  __device__ __forceinline__ DxWave(const DxArgs& args, const uint4* smem) : a(args), lds(smem) {
+    gw = (const uint4*)a.wpack_t;
+    lds_base = (uint32_t)(uintptr_t)(lds_void*)smem;
+    lane = threadIdx.x & 63;
+    wave = threadIdx.x >> 6;
+    h = lane >> 5;
+    wblock = (int64_t)blockIdx.x * P::WAVES + wave;
+    m = wblock * 32 + (lane & 31);
+  }
+
+  template <int g> __device__ __forceinline__ void fetch() {
+    constexpr Group Gr = GT::t.g[g];
+    fetch_group<P, Gr.c0, Gr.nch>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
+  }
+
+  template <int s, int t> __device__ __forceinline__ const Tile& in_tile() const {
+    if constexpr (s == B_RGB) return G;
+    else if constexpr (s == B_V) return Hb[t];
+    else if constexpr (s == B_FA) { if constexpr (t < 8) return Ha[t]; else return DA; }
+    else if constexpr (s == B_7 || s == B_5 || s == B_3 || s == B_1) return Hb[t];
+    else return Ha[t];  // B_6, B_4, B_2
+  }
+  template <int s> __device__ __forceinline__ Tile* out_arr() {
+    if constexpr (s == B_RGB || s == B_FA || s == B_6 || s == B_4 || s == B_2) return Hb;
+    else return Ha;  // B_V, B_7, B_5, B_3, B_1
+  }
+  // (dz tile, mask group or -1) of output tile j of stage s
+  static __host__ __device__ constexpr int dz_tile(int s, int j) {
+    return s == B_RGB ? ZT_V + j : s == B_V ? ZT_F + j : s == B_FA ? ZT_H + 56 + j : ZT_H + 8 * (bwd_fwd_layer(s) - 1) + j;
+  }
+  static __host__ __device__ constexpr int mask_group(int s) {
+    return s == B_RGB ? 8 : s == B_V ? -1 : s == B_FA ? 7 : bwd_fwd_layer(s) - 1;
+  }
+  static __host__ __device__ constexpr int group_stores(int g) { return GT::t.g[g].n * CH; }
+
+  template <int u> __device__ __forceinline__ void unit(uint32_t unit_addr) {
+    constexpr int s = bwd_unit_stage(u), j = u - bwd_unit_first(s);
+    constexpr int T = bwd_in_tiles(s);
+    f32x16 acc;
 #pragma unroll
-  for (int rho = 0; rho < 16; ++rho) P::set(out, rho, ((mask >> rho) & 1u) ? acc[rho] : 0.f);
-  store_tile<P>(a.dz, a.nblk, dz_tile, wblock, lane, out);
-}
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    lds_cu4* w = lds_ptr(unit_addr + (uint32_t)(lane * 16));
+    sfor<T>([&](auto tt) {
+      constexpr int t = decltype(tt)::value;
+      acc = tile_mma<P>(w, t, in_tile<s, t>(), acc);
+    });
+    constexpr int mg = mask_group(s);
+    uint32_t mask = 0xFFFFu;
+    if constexpr (mg >= 0) {
+      const uint32_t w = (j >> 1) == 0 ? mk[mg].x : (j >> 1) == 1 ? mk[mg].y : (j >> 1) == 2 ? mk[mg].z : mk[mg].w;
+      mask = (j & 1) ? (w >> 16) : (w & 0xFFFFu);
+    }
+    Tile out;
+#pragma unroll
+    for (int rho = 0; rho < 16; ++rho) P::set(out, rho, ((mask >> rho) & 1u) ? acc[rho] : 0.f);
+    out_arr<s>()[j] = out;
+    store_tile<P>(a.dz, a.nblk, dz_tile(s, j), wblock, lane, out);
+  }
+
+  template <int g> __device__ __forceinline__ void step() {
+    constexpr Group Gr = GT::t.g[g];
+    constexpr int NG = GT::t.n;
+    if constexpr (g + 1 < NG) fetch<g + 1>();
+    sfor<Gr.n>([&](auto jj) {
+      constexpr int u = Gr.u0 + decltype(jj)::value;
+      unit<u>(lds_base + (uint32_t)(((g % NSLOT) * SLOT_CAP + unit_chunk_off<1>(u, CH) - Gr.c0) * 1024));
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if constexpr (g + 1 < NG) wait_barrier<group_stores(g)>();
+  }
+
+  __device__ __forceinline__ void run() {
+    // output gradients of rgb_linear (rows 0..2) and alpha_linear (row 0): lanes 0..31
+    const float4 gr = m < a.M ? *(const float4*)(a.d_raw + m * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < MASK_GROUPS; ++i) mk[i] = *mask_slot((void*)a.masks, wblock, i, lane);
+    fetch<0>();
+#pragma unroll
+    for (int rho = 0; rho < 16; ++rho) {
+      P::set(G, rho, (h == 0 && rho < 3) ? (rho == 0 ? gr.x : rho == 1 ? gr.y : gr.z) : 0.f);
+      P::set(DA, rho, (h == 0 && rho == 0) ? gr.w : 0.f);
+    }
+    store_tile<P>(a.dz, a.nblk, ZT_RGB, wblock, lane, G);
+    store_tile<P>(a.dz, a.nblk, ZT_A, wblock, lane, DA);
+    wait_barrier<2 * CH>();
+#pragma unroll
+    for (int i = 0; i < MASK_GROUPS; ++i) {
+      settle(mk[i].x);
+      settle(mk[i].y);
+      settle(mk[i].z);
+      settle(mk[i].w);
+    }
+    sfor<GT::t.n>([&](auto gg) { step<decltype(gg)::value>(); });
+  }
+};
 
 template <class P>
 __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
-  using Tile = typename P::Tile;
-  constexpr int SC = dx_slot_chunks<P>();
-  Stream<P, SC> ws{(const uint4*)a.wpack_t, smem_u4, 0};
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 5, c = lane & 31;
-  const int64_t wblock = (int64_t)blockIdx.x * P::WAVES + wave;
-  const int64_t m = wblock * 32 + c;
-
-  f32x16 acc;
-  auto begin = [&](int u) {
-    if (u + 1 < NUNIT_BWD) ws.fetch(bwd_unit_chunk_off(u + 1, P::CH), bwd_unit_chunks(u + 1, P::CH), ws.slot ^ 1);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  };
-  auto end = [&]() {
-    __syncthreads();
-    ws.slot ^= 1;
-  };
-
-  ws.fetch(bwd_unit_chunk_off(0, P::CH), bwd_unit_chunks(0, P::CH), 0);
-
-  // output gradients of rgb_linear (rows 0..2) and alpha_linear (row 0): lanes 0..31
-  const float4 g = m < a.M ? *(const float4*)(a.d_raw + m * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-  Tile G, DA;
-#pragma unroll
-  for (int rho = 0; rho < 16; ++rho) {
-    P::set(G, rho, (h == 0 && rho < 3) ? (rho == 0 ? g.x : rho == 1 ? g.y : g.z) : 0.f);
-    P::set(DA, rho, (h == 0 && rho == 0) ? g.w : 0.f);
-  }
-  store_tile<P>(a.dz, a.nblk, ZT_RGB, wblock, lane, G);
-  store_tile<P>(a.dz, a.nblk, ZT_A, wblock, lane, DA);
-  __syncthreads();
-
-  Tile Ha[8], Hb[8];
-  int unit = 0;
-  // bRGB: dhv = W_rgb^T drgb, masked by hv > 0 -> dZv (Hb[0..3])
-#pragma unroll
-  for (int j = 0; j < 4; ++j, ++unit) {
-    begin(unit);
-    acc = tile_mma<P>(ws.cur(), 0, G, acc, lane);
-    end();
-    dx_finish<P, true>(acc, Hb[j], a, ZT_V + j, 64 + j, m, wblock, h, lane);
-  }
-  // bV: dfeature = W_v[:, :256]^T dZv -> Ha
-#pragma unroll
-  for (int j = 0; j < 8; ++j, ++unit) {
-    begin(unit);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc = tile_mma<P>(ws.cur(), t, Hb[t], acc, lane);
-    end();
-    dx_finish<P, false>(acc, Ha[j], a, ZT_F + j, 0, m, wblock, h, lane);
-  }
-  // bFA: dh7 = W_f^T dfeature + W_a^T dalpha, masked by h7 -> dZ7 (Hb)
-#pragma unroll
-  for (int j = 0; j < 8; ++j, ++unit) {
-    begin(unit);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), t, Ha[t], acc, lane);
-    acc = tile_mma<P>(ws.cur(), 8, DA, acc, lane);
-    end();
-    dx_finish<P, true>(acc, Hb[j], a, ZT_H + 7 * 8 + j, 7 * 8 + j, m, wblock, h, lane);
-  }
-  // b_l (l = 7..1): dh_{l-1} = W_l^T dZ_l (L5: h4 columns only), masked by h_{l-1}
-#define NERF_BWD_LAYER(L, IN, OUT)                                                                \
-  _Pragma("unroll") for (int j = 0; j < 8; ++j, ++unit) {                                         \
-    begin(unit);                                                                                  \
-    _Pragma("unroll") for (int t = 0; t < 8; ++t) acc = tile_mma<P>(ws.cur(), t, IN[t], acc, lane); \
-    end();                                                                                        \
-    dx_finish<P, true>(acc, OUT[j], a, ZT_H + ((L) - 1) * 8 + j, ((L) - 1) * 8 + j, m, wblock, h, lane);       \
-  }
-  NERF_BWD_LAYER(7, Hb, Ha)
-  NERF_BWD_LAYER(6, Ha, Hb)
-  NERF_BWD_LAYER(5, Hb, Ha)
-  NERF_BWD_LAYER(4, Ha, Hb)
-  NERF_BWD_LAYER(3, Hb, Ha)
-  NERF_BWD_LAYER(2, Ha, Hb)
-  NERF_BWD_LAYER(1, Hb, Ha)
-#undef NERF_BWD_LAYER
+  DxWave<P> w(a, smem_u4);
+  w.run();
 }
 
 // ------------------------------------------------------------------------------------
@@ -739,19 +931,44 @@ __global__ void __launch_bounds__(DW_WAVES * 64) dw_kernel(DwArgs a) {
 }  // namespace mlp
 }  // namespace nerf
 
+#ifndef NERF_MLP_DEVICE_ONLY
 // ======================================================================================
 // C-ABI
 // ======================================================================================
 using namespace nerf;
 using namespace nerf::mlp;
 
-template <class P> static constexpr size_t fwd_lds_bytes() { return 2 * (size_t)fwd_slot_chunks<P>() * 1024; }
-template <class P> static constexpr size_t dx_lds_bytes() { return 2 * (size_t)dx_slot_chunks<P>() * 1024; }
+template <class P> static constexpr size_t fwd_lds_bytes() { return (size_t)NSLOT * SLOT_CAP * 1024; }
+template <class P> static constexpr size_t dx_lds_bytes() { return (size_t)NSLOT * SLOT_CAP * 1024; }
 template <class P> static constexpr size_t dw_lds_bytes() { return (size_t)dw_nbuf<P>() * DW_SLOTS * P::CH * 1024; }
 
 template <class K>
 static void allow_lds(K kernel, size_t bytes) {
   if (bytes > 65536) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+template <class P, bool STORE, bool DENSITY>
+static void launch_fwd(const FwdArgs& a, hipStream_t stream) {
+  static const bool lds_ok = (allow_lds(fwd_kernel<P, STORE, DENSITY>, fwd_lds_bytes<P>()), true);
+  (void)lds_ok;
+  const int spb = samples_per_block<P>();
+  dim3 grid((unsigned)(STORE ? a.nblk * 32 / spb : (a.M + spb - 1) / spb));
+  hipLaunchKernelGGL((fwd_kernel<P, STORE, DENSITY>), grid, dim3(P::WAVES * 64), fwd_lds_bytes<P>(), stream, a);
+}
+
+template <class P>
+static void launch_dx(const DxArgs& x, int64_t ldm, hipStream_t stream) {
+  static const bool lds_ok = (allow_lds(dx_kernel<P>, dx_lds_bytes<P>()), true);
+  (void)lds_ok;
+  hipLaunchKernelGGL((dx_kernel<P>), dim3((unsigned)(ldm / samples_per_block<P>())), dim3(P::WAVES * 64),
+                     dx_lds_bytes<P>(), stream, x);
+}
+
+template <class P>
+static void launch_fwd_any(const FwdArgs& a, bool store, bool density, hipStream_t stream) {
+  if (store) launch_fwd<P, true, false>(a, stream);
+  else if (density) launch_fwd<P, false, true>(a, stream);
+  else launch_fwd<P, false, false>(a, stream);
 }
 
 extern "C" {
@@ -771,7 +988,7 @@ int64_t nerf_mlp_act_bytes(int dtype, int64_t M) {
 int64_t nerf_mlp_dz_bytes(int dtype, int64_t M) {
   return (int64_t)Z_ROWS * nerf_mlp_padded_samples(M) * (dtype == 0 ? 4 : 2);
 }
-int64_t nerf_mlp_mask_bytes(int64_t M) { return nerf_mlp_padded_samples(M) / 32 * MASK_TILES * 64 * 2; }
+int64_t nerf_mlp_mask_bytes(int64_t M) { return nerf_mlp_padded_samples(M) / 32 * MASK_GROUPS * 64 * 16; }
 
 int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void* packed_bwd, hipStream_t stream) {
   NERF_REQUIRE(params != nullptr, "nerf_mlp_pack: params is null");
@@ -788,11 +1005,11 @@ int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void*
     const int64_t n = total_chunks(ch, dir) * 64;
     dim3 grid((unsigned)((n + 255) / 256));
     if (dtype == 0) {
-      if (dir == 0) hipLaunchKernelGGL((pack_kernel<PF32, 0>), grid, dim3(256), 0, stream, prm, (char*)dst);
-      else hipLaunchKernelGGL((pack_kernel<PF32, 1>), grid, dim3(256), 0, stream, prm, (char*)dst);
+      if (dir == 0) hipLaunchKernelGGL((pack_kernel<PF32, 0>), grid, dim3(256), 0, stream, prm, unit_offsets<PF32::CH, 0>(), (char*)dst);
+      else hipLaunchKernelGGL((pack_kernel<PF32, 1>), grid, dim3(256), 0, stream, prm, unit_offsets<PF32::CH, 1>(), (char*)dst);
     } else {
-      if (dir == 0) hipLaunchKernelGGL((pack_kernel<PBF16, 0>), grid, dim3(256), 0, stream, prm, (char*)dst);
-      else hipLaunchKernelGGL((pack_kernel<PBF16, 1>), grid, dim3(256), 0, stream, prm, (char*)dst);
+      if (dir == 0) hipLaunchKernelGGL((pack_kernel<PBF16, 0>), grid, dim3(256), 0, stream, prm, unit_offsets<PBF16::CH, 0>(), (char*)dst);
+      else hipLaunchKernelGGL((pack_kernel<PBF16, 1>), grid, dim3(256), 0, stream, prm, unit_offsets<PBF16::CH, 1>(), (char*)dst);
     }
     if (int e = check_launch("nerf_mlp_pack")) return e;
   }
@@ -814,30 +1031,8 @@ int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const floa
   NERF_REQUIRE(!(store && density), "nerf_mlp_fwd: store and density-only are exclusive");
   FwdArgs a{(const char*)packed_fwd, pts, viewdirs, dir_index, samples_per_dir, M,
             nerf_mlp_padded_samples(M) / 32, raw, act, masks};
-  if (dtype == 0) {
-    using P = PF32;
-    const int spb = samples_per_block<P>();
-    dim3 grid((unsigned)(store ? a.nblk * 32 / spb : (M + spb - 1) / spb));
-    const size_t lds = fwd_lds_bytes<P>();
-    if (store) {
-      allow_lds(fwd_kernel<P, true, false>, lds);
-      hipLaunchKernelGGL((fwd_kernel<P, true, false>), grid, dim3(P::WAVES * 64), lds, stream, a);
-    } else if (density) {
-      allow_lds(fwd_kernel<P, false, true>, lds);
-      hipLaunchKernelGGL((fwd_kernel<P, false, true>), grid, dim3(P::WAVES * 64), lds, stream, a);
-    } else {
-      allow_lds(fwd_kernel<P, false, false>, lds);
-      hipLaunchKernelGGL((fwd_kernel<P, false, false>), grid, dim3(P::WAVES * 64), lds, stream, a);
-    }
-  } else {
-    using P = PBF16;
-    const int spb = samples_per_block<P>();
-    dim3 grid((unsigned)(store ? a.nblk * 32 / spb : (M + spb - 1) / spb));
-    const size_t lds = fwd_lds_bytes<P>();
-    if (store) hipLaunchKernelGGL((fwd_kernel<P, true, false>), grid, dim3(P::WAVES * 64), lds, stream, a);
-    else if (density) hipLaunchKernelGGL((fwd_kernel<P, false, true>), grid, dim3(P::WAVES * 64), lds, stream, a);
-    else hipLaunchKernelGGL((fwd_kernel<P, false, false>), grid, dim3(P::WAVES * 64), lds, stream, a);
-  }
+  if (dtype == 0) launch_fwd_any<PF32>(a, store, density, stream);
+  else launch_fwd_any<PBF16>(a, store, density, stream);
   return check_launch("nerf_mlp_fwd");
 }
 
@@ -858,16 +1053,8 @@ int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64
   NERF_REQUIRE(packed_bwd && d_raw && masks && dz, "nerf_mlp_bwd_dx: null pointer");
   const int64_t ldm = nerf_mlp_padded_samples(M);
   DxArgs x{(const char*)packed_bwd, d_raw, M, ldm / 32, masks, dz};
-  if (dtype == 0) {
-    using P = PF32;
-    allow_lds(dx_kernel<P>, dx_lds_bytes<P>());
-    hipLaunchKernelGGL((dx_kernel<P>), dim3((unsigned)(ldm / samples_per_block<P>())), dim3(P::WAVES * 64),
-                       dx_lds_bytes<P>(), stream, x);
-  } else {
-    using P = PBF16;
-    hipLaunchKernelGGL((dx_kernel<P>), dim3((unsigned)(ldm / samples_per_block<P>())), dim3(P::WAVES * 64),
-                       dx_lds_bytes<P>(), stream, x);
-  }
+  if (dtype == 0) launch_dx<PF32>(x, ldm, stream);
+  else launch_dx<PBF16>(x, ldm, stream);
   return check_launch("nerf_mlp_bwd_dx");
 }
 
@@ -899,3 +1086,4 @@ int nerf_mlp_bwd(const void* packed_bwd, int dtype, const float* d_raw, int64_t 
 }
 
 }  // extern "C"
+#endif  // NERF_MLP_DEVICE_ONLY

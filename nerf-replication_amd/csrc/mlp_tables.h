@@ -150,8 +150,9 @@ enum DzTile {
 };
 constexpr int A_ROWS = AT_TILES * 32;  // 2528 feature rows
 constexpr int Z_ROWS = ZT_TILES * 32;  // 2496
-// ReLU masks: per 32-sample wave block, 68 tiles x 64 lanes x 16 bits
-constexpr int MASK_TILES = 68;  // h0..h7 (8x8), hv (4)
+// ReLU masks: per 32-sample wave block, 9 groups x 64 lanes x 16 B (layers h0..h7: 8 tiles x
+// 16 bits each; group 8: the 4 view-layer tiles)
+constexpr int MASK_GROUPS = 9;
 
 // dW GEMM list (per net): C[n][k] = sum_m dz[n][m] act[k][m]
 constexpr int NGEMM = 12;

@@ -1,0 +1,92 @@
+"""Microbenchmark of the MLP kernels alone (no renderer), for kernel iteration.
+
+    python tools/mlp_bench.py [--M 786432] [--reps 10] [--dtype bf16]
+
+Times nerf_mlp_fwd (inference and training store), nerf_mlp_bwd_dx, nerf_mlp_bwd_dw and
+nerf_mlp_pack with HIP events on the launching stream and prints one JSON line with
+ms and TFLOP/s per kernel (algorithmic FLOP).
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "nerf-replication_amd"))
+
+import torch  # noqa: E402
+
+from nerf_amd import _lib, ops  # noqa: E402
+from nerf_amd._lib import check, lib, ptr, stream_of  # noqa: E402
+
+FLOP = {"fwd": 2 * 593408, "fwd_train": 2 * 593408, "dx": 2 * 557696, "dw": 2 * 593408, "density": 2 * 491264}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=786432)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--lib", default=None, help="alternative build of libnerf_amd.so (kernel experiments)")
+    args = ap.parse_args()
+    if args.lib:
+        _lib.LIB_PATH = os.path.abspath(args.lib)
+    dev = torch.device("cuda:0")
+    dt = ops.dtype_code(args.dtype)
+    torch.manual_seed(0)
+    shapes = [(256, 63), (256,)] + [(256, 256), (256,)] * 4 + [(256, 319), (256,)] + [(256, 256), (256,)] * 2 + \
+             [(128, 283), (128,), (256, 256), (256,), (1, 256), (1,), (3, 128), (3,)]
+    params = [(torch.rand(s, device=dev) - 0.5) * (0.2 if len(s) == 2 else 0.1) for s in shapes]
+    packer = ops.PackedMLP(params)
+    L = lib()
+    M = args.M
+    pts = (torch.rand(M, 3, device=dev) - 0.5) * 3
+    vd = torch.nn.functional.normalize(torch.randn(M // 192 + 1, 3, device=dev), dim=-1)
+    raw = torch.empty(M, 4, device=dev)
+    act = torch.empty(L.nerf_mlp_act_bytes(dt, M), dtype=torch.uint8, device=dev)
+    masks = torch.empty(L.nerf_mlp_mask_bytes(M), dtype=torch.uint8, device=dev)
+    dz = torch.empty(L.nerf_mlp_dz_bytes(dt, M), dtype=torch.uint8, device=dev)
+    grad = torch.zeros(L.nerf_mlp_net_params(), device=dev)
+    d_raw = torch.randn(M, 4, device=dev) * 1e-3
+    pf, pb = packer.get(dt, 0), packer.get(dt, 1)
+    s = stream_of(pts)
+    arr = None
+
+    def pack():
+        import ctypes
+        nonlocal arr
+        arr = ctypes.cast((ctypes.c_void_p * 24)(*[p.data_ptr() for p in params]), ctypes.c_void_p)
+        check(L.nerf_mlp_pack(arr, dt, ptr(pf), ptr(pb), s), "pack")
+
+    kern = {
+        "fwd": lambda: check(L.nerf_mlp_fwd(ptr(pf), dt, ptr(pts), ptr(vd), 192, None, M, 0, ptr(raw), None, None, s),
+                             "fwd"),
+        "fwd_train": lambda: check(L.nerf_mlp_fwd(ptr(pf), dt, ptr(pts), ptr(vd), 192, None, M, 1, ptr(raw), ptr(act),
+                                                  ptr(masks), s), "fwd_train"),
+        "dx": lambda: check(L.nerf_mlp_bwd_dx(ptr(pb), dt, ptr(d_raw), M, ptr(masks), ptr(dz), s), "dx"),
+        "dw": lambda: check(L.nerf_mlp_bwd_dw(dt, M, ptr(act), ptr(dz), ptr(grad), s), "dw"),
+        "density": lambda: check(L.nerf_mlp_fwd(ptr(pf), dt, ptr(pts), None, 1, None, M, 2, ptr(raw), None, None, s),
+                                 "density"),
+        "pack": pack,
+    }
+    out = {"M": M, "dtype": args.dtype}
+    for name, fn in kern.items():
+        fn()
+        torch.cuda.synchronize()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(args.reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / args.reps
+        ent = {"ms": round(ms, 4)}
+        if name in FLOP:
+            ent["tflops"] = round(FLOP[name] * M / (ms * 1e-3) / 1e12, 1)
+        out[name] = ent
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
