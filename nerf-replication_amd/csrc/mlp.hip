@@ -227,6 +227,9 @@ __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 constexpr int SLOT_CAP = 72;   // KiB (1 KiB chunks) per ring slot: 2 x 72 KiB of 160 KiB LDS
 constexpr int NSLOT = 2;
 constexpr int GROUP_MAX = 8;   // units per group
+#ifndef NERF_GROUP_ACROSS
+#define NERF_GROUP_ACROSS 1    // groups may span layers: every group fills its slot
+#endif
 
 struct Group { int u0, n, c0, nch; };  // first unit, units, first chunk, chunks
 
@@ -261,7 +264,8 @@ struct Groups {
       }
       Group G{u, 0, unit_chunk_off<DIR>(u, CH), 0};
       const int seg = unit_seg<DIR>(u);
-      while (u < NU && unit_used<DIR, DENSITY>(u) && unit_seg<DIR>(u) == seg && G.n < GROUP_MAX &&
+      while (u < NU && unit_used<DIR, DENSITY>(u) && (NERF_GROUP_ACROSS || unit_seg<DIR>(u) == seg) &&
+             G.n < GROUP_MAX &&
              G.nch + unit_chunks<DIR>(u, CH) <= SLOT_CAP) {
         G.nch += unit_chunks<DIR>(u, CH);
         ++G.n;
@@ -378,10 +382,26 @@ __device__ __forceinline__ void pe_tile(typename P::Tile& t, int h, float x0, fl
 
 // fragment-native store of one finished tile (mlp_tables.h, "Training stores"): CH
 // lane-linear 16-byte stores per lane, each wave-instruction writes 1 KiB contiguous
+#ifndef NERF_BLOCK_MAJOR
+#define NERF_BLOCK_MAJOR 1
+#endif
+// KiB offset of chunk c of tile tau of 32-sample block b in a store of `ntiles` tiles.
+// Block-major: one block's tiles are contiguous (a dW job reads a few contiguous runs per
+// block instead of one 1-2 KiB piece from each of up to 18 distant tile planes).
+__host__ __device__ constexpr int64_t tile_kib(int64_t nblk, int ntiles, int tau, int64_t b, int c, int ch) {
+  return NERF_BLOCK_MAJOR ? ((b * ntiles + tau) * ch + c) : (((int64_t)tau * nblk + b) * ch + c);
+}
+// KiB stride between consecutive blocks of one tile
+__host__ __device__ constexpr int64_t block_stride_kib(int ntiles, int ch) {
+  return NERF_BLOCK_MAJOR ? (int64_t)ntiles * ch : ch;
+}
+
+// fragment-native store of one finished tile (mlp_tables.h, "Training stores"): CH
+// lane-linear 16-byte stores per lane, each wave-instruction writes 1 KiB contiguous
 template <class P>
-__device__ __forceinline__ void store_tile(void* base, int64_t nblk, int tau, int64_t wblock, int lane,
+__device__ __forceinline__ void store_tile(void* base, int64_t nblk, int ntiles, int tau, int64_t wblock, int lane,
                                            const typename P::Tile& t) {
-  uint4* dst = (uint4*)base + ((int64_t)tau * nblk + wblock) * P::CH * 64 + lane;
+  uint4* dst = (uint4*)base + tile_kib(nblk, ntiles, tau, wblock, 0, P::CH) * 64 + lane;
 #pragma unroll
   for (int c = 0; c < P::CH; ++c) dst[c * 64] = P::chunk(t, c);
 }
@@ -498,7 +518,7 @@ struct FwdWave {
       }
       out_arr<L>()[n] = out;
       if constexpr (STORE) {
-        store_tile<P>(a.act, a.nblk, (L == LV ? AT_V : AT_H + 8 * L) + n, wblock, lane, out);
+        store_tile<P>(a.act, a.nblk, AT_TILES, (L == LV ? AT_V : AT_H + 8 * L) + n, wblock, lane, out);
         if constexpr ((n & 1) == 0) mw[n >> 1] = bits;
         else mw[n >> 1] |= bits << 16;
         if constexpr (n == fwd_out_tiles(L) - 1)
@@ -511,7 +531,7 @@ struct FwdWave {
 #pragma unroll
         for (int rho = 0; rho < 16; ++rho) P::set(out, rho, acc[rho]);
         Ha[n] = out;
-        if constexpr (STORE) store_tile<P>(a.act, a.nblk, AT_F + n, wblock, lane, out);
+        if constexpr (STORE) store_tile<P>(a.act, a.nblk, AT_TILES, AT_F + n, wblock, lane, out);
       } else {
         alpha = acc[0];  // alpha_linear: output row 0 = register 0 of lanes 0..31
       }
@@ -553,7 +573,8 @@ struct FwdWave {
     if constexpr (g + 1 < NG) fetch<g + 1>();
     sfor<G.n>([&](auto jj) {
       constexpr int u = G.u0 + decltype(jj)::value;
-      unit<u>(lds_base + (uint32_t)(((g % NSLOT) * SLOT_CAP + unit_chunk_off<0>(u, CH) - G.c0) * 1024));
+      constexpr int off = (g % NSLOT) * SLOT_CAP + unit_chunk_off<0>(u, CH) - G.c0;  // compile time
+      unit<u>(lds_base + (uint32_t)(off * 1024));
       // one scheduling region per unit: hipcc would otherwise hoist every LDS read of the
       // group (up to 256 VGPRs of A operands) to its top and spill
       __builtin_amdgcn_sched_barrier(0);
@@ -579,9 +600,9 @@ struct FwdWave {
     if constexpr (STORE) {
       Tile Dt;
       pe_tile<P, 0, 4, 27>(Dt, h, dx, dy, dz);
-      store_tile<P>(a.act, a.nblk, AT_X, wblock, lane, X[0]);
-      store_tile<P>(a.act, a.nblk, AT_X + 1, wblock, lane, X[1]);
-      store_tile<P>(a.act, a.nblk, AT_D, wblock, lane, Dt);
+      store_tile<P>(a.act, a.nblk, AT_TILES, AT_X, wblock, lane, X[0]);
+      store_tile<P>(a.act, a.nblk, AT_TILES, AT_X + 1, wblock, lane, X[1]);
+      store_tile<P>(a.act, a.nblk, AT_TILES, AT_D, wblock, lane, Dt);
     }
     wait_barrier<STORE ? 3 * CH : 0>();
     settle(dx);
@@ -684,7 +705,8 @@ struct DxWave {
 #pragma unroll
     for (int rho = 0; rho < 16; ++rho) P::set(out, rho, ((mask >> rho) & 1u) ? acc[rho] : 0.f);
     out_arr<s>()[j] = out;
-    store_tile<P>(a.dz, a.nblk, dz_tile(s, j), wblock, lane, out);
+    constexpr int dzt = dz_tile(s, j);
+    store_tile<P>(a.dz, a.nblk, ZT_TILES, dzt, wblock, lane, out);
   }
 
   template <int g> __device__ __forceinline__ void step() {
@@ -693,7 +715,8 @@ struct DxWave {
     if constexpr (g + 1 < NG) fetch<g + 1>();
     sfor<Gr.n>([&](auto jj) {
       constexpr int u = Gr.u0 + decltype(jj)::value;
-      unit<u>(lds_base + (uint32_t)(((g % NSLOT) * SLOT_CAP + unit_chunk_off<1>(u, CH) - Gr.c0) * 1024));
+      constexpr int off = (g % NSLOT) * SLOT_CAP + unit_chunk_off<1>(u, CH) - Gr.c0;  // compile time
+      unit<u>(lds_base + (uint32_t)(off * 1024));
       __builtin_amdgcn_sched_barrier(0);
     });
     if constexpr (g + 1 < NG) wait_barrier<group_stores(g)>();
@@ -710,8 +733,8 @@ struct DxWave {
       P::set(G, rho, (h == 0 && rho < 3) ? (rho == 0 ? gr.x : rho == 1 ? gr.y : gr.z) : 0.f);
       P::set(DA, rho, (h == 0 && rho == 0) ? gr.w : 0.f);
     }
-    store_tile<P>(a.dz, a.nblk, ZT_RGB, wblock, lane, G);
-    store_tile<P>(a.dz, a.nblk, ZT_A, wblock, lane, DA);
+    store_tile<P>(a.dz, a.nblk, ZT_TILES, ZT_RGB, wblock, lane, G);
+    store_tile<P>(a.dz, a.nblk, ZT_TILES, ZT_A, wblock, lane, DA);
     wait_barrier<2 * CH>();
 #pragma unroll
     for (int i = 0; i < MASK_GROUPS; ++i) {
@@ -732,58 +755,90 @@ __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
-// dW / db: C[n][k] += sum_m dz[n][m] act[k][m] over a chunk of 32-sample blocks.
-// job = (gemm g, n-group, k-group, block chunk); wave w owns n-tile w of the group and
-// accumulates all (<= 8) k-tiles of the group.  Per block, the group's dz and act
-// tile-blocks (fragment-native, mlp_tables.h) are copied to LDS with global_load_lds and
-// read back transposed: K = samples.  Row i of a fragment <-> feature acc_row(i&15, i>>4).
+// dW / db: C[n][k] += sum_m dz[n][m] act[k][m] (K = samples), one pass over the stores.
+//
+// Ten jobs, each reading every tile it needs once per 32-sample block (159 tile-blocks per
+// block for the whole net):
+//   J0..J7  pts_linears.l: 8 dZ_l tiles x (2 | 8 | 10) act tiles; wave w owns n-tile w
+//   J8      feature_linear (8 dF x 8 h7) + alpha_linear (dA x h7): wave w also owns the
+//           alpha row against h7 tile w
+//   J9      views_linears (4 dZv x [8 feature, PE(dir)]) on waves 0..3 + rgb_linear
+//           (d rgb x hv tile w-4) on waves 4..7
+// Work items = (job, contiguous block range) sized to equal bytes, as many as there are
+// CUs (nerf_mlp_dw_items), so the single wave of workgroups ends together.  Per block, a
+// job's tile-blocks (fragment-native, mlp_tables.h) stream into an LDS ring with LDS-DMA
+// and are read back transposed (ds_read_b64_tr_b16): row i of a fragment <-> feature
+// acc_row(i & 15, i >> 4).  Each item adds its partial sums with fp32 atomics.
 // ------------------------------------------------------------------------------------
+constexpr int DW_WAVES = 8;
+constexpr int DW_SLOTS = 18;  // most tile-blocks one job reads per block
+constexpr int NDWJOB = 10;
+enum DwKind { DW_REG = 0, DW_FA = 1, DW_VR = 2 };
+
+struct DwJobDesc {
+  int kind, kt;     // kind; k-tiles per wave (REG / FA trunk / VR view waves)
+  int nd, na;       // dz tiles, act tiles (LDS slots [0, nd) then [nd, nd + na))
+  int dz[9];        // dz tile ids
+  int act[13];      // act tile ids
+};
+__host__ __device__ constexpr DwJobDesc dw_job_desc(int j) {
+  DwJobDesc d{};
+  if (j < 8) {
+    d.kind = DW_REG;
+    d.kt = gemm_k_tiles(j);
+    d.nd = 8;
+    d.na = d.kt;
+    for (int n = 0; n < 8; ++n) d.dz[n] = ZT_H + 8 * j + n;
+    for (int t = 0; t < d.kt; ++t) d.act[t] = gemm_act_tile(j, t);
+  } else if (j == 8) {
+    d.kind = DW_FA;
+    d.kt = 8;
+    d.nd = 9;
+    d.na = 8;
+    for (int n = 0; n < 8; ++n) d.dz[n] = ZT_F + n;
+    d.dz[8] = ZT_A;
+    for (int t = 0; t < 8; ++t) d.act[t] = AT_H + 56 + t;
+  } else {
+    d.kind = DW_VR;
+    d.kt = 9;
+    d.nd = 5;
+    d.na = 13;
+    for (int n = 0; n < 4; ++n) d.dz[n] = ZT_V + n;
+    d.dz[4] = ZT_RGB;
+    for (int t = 0; t < 8; ++t) d.act[t] = AT_F + t;
+    d.act[8] = AT_D;
+    for (int t = 0; t < 4; ++t) d.act[9 + t] = AT_V + t;
+  }
+  return d;
+}
+__host__ __device__ constexpr int dw_job_tiles(int j) { return dw_job_desc(j).nd + dw_job_desc(j).na; }
+
+// LDS ring depth: 4 x 36 KiB (bf16), 2 x 72 KiB (fp32)
+#ifndef NERF_DW_NBUF_BF16
+#define NERF_DW_NBUF_BF16 4
+#endif
+template <class P> __host__ __device__ constexpr int dw_nbuf() { return P::CH == 2 ? NERF_DW_NBUF_BF16 : 2; }
+__host__ __device__ constexpr int perm_row(int i) { return acc_row(i & 15, i >> 4); }
+
+// work items: item_off[j] = first item of job j (item_off[NDWJOB] = total)
 struct DwArgs {
   const void* dz;
   const void* act;
   int64_t nblk;       // 32-sample blocks in the stores
-  int64_t chunk_blk;  // blocks per job
-  int nchunks;
   float* grad;        // flat [NET_PARAMS], accumulated
+  int item_off[NDWJOB + 1];
 };
 
-struct DwJob { int g, ng, kg; };
-
-__host__ __device__ constexpr int gemm_ngroups(int g) { return (gemm_n_tiles(g) + 7) / 8; }
-__host__ __device__ constexpr int gemm_kgroups(int g) { return (gemm_k_tiles(g) + 7) / 8; }
-__host__ __device__ constexpr int n_dw_jobs_per_chunk() {
-  int n = 0;
-  for (int g = 0; g < NGEMM; ++g) n += gemm_ngroups(g) * gemm_kgroups(g);
-  return n;
-}
-__device__ __forceinline__ DwJob dw_job(int j) {
-  for (int g = 0; g < NGEMM; ++g) {
-    const int n = gemm_ngroups(g) * gemm_kgroups(g);
-    if (j < n) return DwJob{g, j / gemm_kgroups(g), j % gemm_kgroups(g)};
-    j -= n;
-  }
-  return DwJob{0, 0, 0};
-}
-
-constexpr int DW_WAVES = 8;
-constexpr int DW_SLOTS = 16;  // 8 dz tiles + 8 act tiles per block
-__host__ __device__ constexpr int perm_row(int i) { return acc_row(i & 15, i >> 4); }
-// LDS ring depth: 3 x 32 KiB (bf16), 2 x 64 KiB (fp32) -- both within 160 KiB
-template <class P> __host__ __device__ constexpr int dw_nbuf() { return P::CH == 2 ? 3 : 2; }
-
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n in [0, 8]
-__device__ __forceinline__ void wait_vmcnt(int n) {
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n in [0, 63] (n is a multiple of G here)
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+#define NERF_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
   switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    NERF_VMW(0) NERF_VMW(1) NERF_VMW(2) NERF_VMW(3) NERF_VMW(4) NERF_VMW(5) NERF_VMW(6) NERF_VMW(7)
+    NERF_VMW(8) NERF_VMW(9) NERF_VMW(10) NERF_VMW(11) NERF_VMW(12) NERF_VMW(13) NERF_VMW(14) NERF_VMW(15)
+    NERF_VMW(16) NERF_VMW(17) NERF_VMW(18)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
+#undef NERF_VMW
 }
 
 typedef __attribute__((ext_vector_type(4))) short short4_t;
@@ -806,125 +861,181 @@ __device__ __forceinline__ float dw_frag_f32(const char* tile, int s, int lane) 
   return *(const float*)(tile + (rho >> 2) * 1024 + (2 * s + h + 32 * hp) * 16 + (rho & 3) * 4);
 }
 
+// one K step (16 samples bf16 / 2 samples fp32) of C += A B^T for A = LDS tile `at`
 template <class P>
-__global__ void __launch_bounds__(DW_WAVES * 64) dw_kernel(DwArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
-  constexpr int TB = P::CH * 1024;           // tile-block bytes
-  constexpr int BUF = DW_SLOTS * TB;         // one block's tiles
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int chunk_id = blockIdx.x % a.nchunks;
-  const DwJob job = dw_job(blockIdx.x / a.nchunks);
-  const int g = job.g;
-  const int nt0 = job.ng * 8, kt0 = job.kg * 8;
-  const int ntiles = min(8, gemm_n_tiles(g) - nt0);
-  const int ktiles = min(8, gemm_k_tiles(g) - kt0);
-  const bool active = wave < ntiles;
-  const int64_t b_begin = (int64_t)chunk_id * a.chunk_blk;
-  const int64_t b_end = min(b_begin + a.chunk_blk, a.nblk);
-  char* lds = (char*)smem_u4;
-
-  // copy one block's tile-blocks into buffer `buf` (each wave-instruction = 1 KiB).  Wave w
-  // issues chunks k = w, w + 8, ... (G of them); their sources and LDS offsets are resolved
-  // once here -- a table lookup inside the loop would be an ordinary global load, whose
-  // compiler wait is vmcnt(0) and drains the ring.
-  const int nchunk = (ntiles + ktiles) * P::CH;
-  constexpr int GMAX = 16 * P::CH / DW_WAVES;
-  const int G = wave < nchunk ? (nchunk - wave + DW_WAVES - 1) / DW_WAVES : 0;
-  const char* src[GMAX];
-  int dst[GMAX];
+__device__ __forceinline__ f32x16 dw_mma(const char* at, const char* bt, int s, int lane, f32x16 acc) {
+  if constexpr (P::CH == 2)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(dw_frag_bf16(at, s, lane), dw_frag_bf16(bt, s, lane), acc, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(dw_frag_f32(at, s, lane), dw_frag_f32(bt, s, lane), acc, 0, 0, 0);
+}
+template <class P>
+__device__ __forceinline__ float dw_rowsum(const char* at, int s, int lane) {
+  if constexpr (P::CH == 2) {
+    const bf16x8 v = dw_frag_bf16(at, s, lane);
+    float r = 0.f;
 #pragma unroll
-  for (int i = 0; i < GMAX; ++i) {
-    const int k = wave + DW_WAVES * i;
-    const int which = k / P::CH, c = k % P::CH;
-    const bool is_a = which < ntiles;
-    const int slot = is_a ? which : 8 + (which - ntiles);
-    const int tau = k >= nchunk ? 0 : is_a ? gemm_dz_tile(g, nt0 + which) : gemm_act_tile(g, kt0 + which - ntiles);
-    src[i] = (const char*)(is_a ? a.dz : a.act) + ((int64_t)tau * a.nblk * P::CH + c) * 1024 + lane * 16;
-    dst[i] = slot * TB + c * 1024;
+    for (int e = 0; e < 8; ++e) r += (float)v[e];
+    return r;
+  } else {
+    return dw_frag_f32(at, s, lane);
+  }
+}
+
+// add a 32 x 32 accumulator tile into weight WP at rows 32 ntile + perm, columns col0 +
+// perm (valid rows < nvalid, valid columns < cvalid of the tile).  The layout functions
+// are loops: every use sits in a constant expression.
+template <int WP>
+__device__ __forceinline__ void dw_flush(float* grad, int ntile, int nvalid, int col0, int cvalid, const f32x16& acc,
+                                         int lane) {
+  constexpr int64_t OFF = param_offset(WP);
+  constexpr int K = weight_K(WP);
+  float* gw = grad + OFF;
+  const int h = lane >> 5, colf = perm_row(lane & 31);
+  if (colf >= cvalid) return;
+#pragma unroll
+  for (int rho = 0; rho < 16; ++rho) {
+    const int n = 32 * ntile + perm_row(acc_row(rho, h));
+    if (n < nvalid) atomicAdd(gw + (int64_t)n * K + col0 + colf, acc[rho]);
+  }
+}
+template <int WPB>
+__device__ __forceinline__ void dw_flush_bias(float* grad, int ntile, int nvalid, float dbias, int lane) {
+  constexpr int64_t OFF = param_offset(WPB);
+  dbias += __shfl_xor(dbias, 32, 64);
+  const int n = 32 * ntile + perm_row(lane & 31);
+  if (lane < 32 && n < nvalid) atomicAdd(grad + OFF + n, dbias);
+}
+
+template <class P, int J>
+__device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t b_end, char* lds) {
+  constexpr DwJobDesc JD = dw_job_desc(J);
+  constexpr int TB = P::CH * 1024;            // tile-block bytes
+  constexpr int BUF = DW_SLOTS * TB;          // one stage of the ring
+  constexpr int NT = JD.nd + JD.na;
+  constexpr int NCHUNK = NT * P::CH;
+  constexpr int G = (NCHUNK + DW_WAVES - 1) / DW_WAVES;  // DMA per wave per block (uniform)
+  constexpr int NBUF = dw_nbuf<P>(), D = NBUF - 1;
+  constexpr int KS = P::CH == 2 ? 2 : 16;    // K steps per 32-sample block
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+  // DMA sources / LDS offsets, resolved once (a table lookup inside the loop would be a
+  // compiler-visible load, whose wait drains the ring)
+  const char* src[G];
+  uint32_t dst[G];
+  int64_t bstride[G];
+#pragma unroll
+  for (int i = 0; i < G; ++i) {
+    const int k = cmin(wave + DW_WAVES * i, NCHUNK - 1);
+    const int slot = k / P::CH, c = k % P::CH;
+    const bool is_dz = slot < JD.nd;
+    int tau = 0;
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+      if (q == slot) tau = q < JD.nd ? JD.dz[q] : JD.act[q - JD.nd];
+    const int ntiles = is_dz ? ZT_TILES : AT_TILES;
+    src[i] = (const char*)(is_dz ? a.dz : a.act) + tile_kib(a.nblk, ntiles, tau, 0, c, P::CH) * 1024 + lane * 16;
+    bstride[i] = block_stride_kib(ntiles, P::CH) * 1024;
+    dst[i] = (uint32_t)(slot * TB + c * 1024);
   }
   const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_void*)lds;
   auto fetch = [&](int64_t b, int buf) {
-    const int64_t boff = b * (P::CH * 1024);
 #pragma unroll
-    for (int i = 0; i < GMAX; ++i)
-      if (i < G) glds16_asm(src[i] + boff, lds_base + buf * BUF + dst[i]);
+    for (int i = 0; i < G; ++i) glds16_asm(src[i] + b * bstride[i], lds_base + (uint32_t)(buf * BUF) + dst[i]);
   };
 
-  f32x16 acc[8];
+  // wave roles
+  //   REG: n slot w, k slots nd .. nd + kt;  FA: + alpha (slot 8) x k slot nd + w
+  //   VR: waves 0..3 n slot w, k slots nd .. nd + 9; waves 4..7 n slot 4 (d rgb) x slot nd + 9 + (w - 4)
+  const bool vr_rgb = JD.kind == DW_VR && wave >= 4;
+  const int n_slot = vr_rgb ? 4 : wave;
+  f32x16 acc[10], acc2;
 #pragma unroll
-  for (int t = 0; t < 8; ++t)
+  for (int t = 0; t < 10; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-  float dbias = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc2[i] = 0.f;
+  float dbias = 0.f, dbias2 = 0.f;
 
-  // NBUF-slot ring, D = NBUF - 1 blocks in flight: per block each wave issues the same
-  // number G of global_load_lds, so "block b landed" = vmcnt(G * younger blocks in flight),
-  // then a raw s_barrier -- no vmcnt(0) drain (cdna_hip_programming.md, LDS-DMA ordering).
-  constexpr int NBUF = dw_nbuf<P>(), D = NBUF - 1;
   for (int d = 0; d < D; ++d)
     if (b_begin + d < b_end) fetch(b_begin + d, d);
   int buf = 0;
   for (int64_t b = b_begin; b < b_end; ++b) {
     const int younger = (int)min((int64_t)(D - 1), b_end - 1 - b);
-    wait_vmcnt(G * younger);
+    wait_vmcnt_rt(G * younger);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (b + D < b_end) fetch(b + D, buf == 0 ? NBUF - 1 : buf - 1);
-    if (active) {
-      const char* tiles = lds + buf * BUF;
-      const char* at = tiles + wave * TB;
-      if constexpr (P::CH == 2) {
+    const char* tiles = lds + buf * BUF;
+    const char* nt = tiles + n_slot * TB;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const bf16x8 af = dw_frag_bf16(at, s, lane);
+    for (int s = 0; s < KS; ++s) {
+      if (!vr_rgb) {
+        dbias += dw_rowsum<P>(nt, s, lane);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) dbias += (float)af[e];
-#pragma unroll
-          for (int t = 0; t < 8; ++t)
-            if (t < ktiles)
-              acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, dw_frag_bf16(tiles + (8 + t) * TB, s, lane), acc[t],
-                                                               0, 0, 0);
-        }
+        for (int t = 0; t < JD.kt; ++t) acc[t] = dw_mma<P>(nt, tiles + (JD.nd + t) * TB, s, lane, acc[t]);
       } else {
-#pragma unroll 4
-        for (int s = 0; s < 16; ++s) {
-          const float af = dw_frag_f32(at, s, lane);
-          dbias += af;
-#pragma unroll
-          for (int t = 0; t < 8; ++t)
-            if (t < ktiles)
-              acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af, dw_frag_f32(tiles + (8 + t) * TB, s, lane), acc[t], 0,
-                                                            0, 0);
-        }
+        dbias += dw_rowsum<P>(nt, s, lane);
+        acc[0] = dw_mma<P>(nt, tiles + (JD.nd + 9 + (wave - 4)) * TB, s, lane, acc[0]);
+      }
+      if constexpr (JD.kind == DW_FA) {
+        const char* at = tiles + 8 * TB;
+        if (wave == 0) dbias2 += dw_rowsum<P>(at, s, lane);
+        acc2 = dw_mma<P>(at, tiles + (JD.nd + wave) * TB, s, lane, acc2);
       }
     }
     buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
-  if (!active) return;
-  // accumulate into the flat gradient (state_dict layout: weight [N][K] row-major)
-  const int wp = gemm_weight(g);
-  float* gw = a.grad + param_offset(wp);
-  const int K = weight_K(wp);
-  const int nvalid = gemm_n_valid(g);
-  const int h = lane >> 5, j = lane & 31;
+
+  // flush (state_dict layout: weight [N][K] row-major)
+  if constexpr (JD.kind == DW_REG) {
+    constexpr int WP = gemm_weight(J);
+    sfor<JD.kt>([&](auto tt) {
+      constexpr int t = decltype(tt)::value;
+      constexpr int C0 = gemm_col0(J, t), CV = gemm_col_valid(J, t);
+      dw_flush<WP>(a.grad, wave, 256, C0, CV, acc[t], lane);
+    });
+    dw_flush_bias<WP + 1>(a.grad, wave, 256, dbias, lane);
+  } else if constexpr (JD.kind == DW_FA) {
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    if (t < ktiles) {
-      const int kt = kt0 + t;
-      const int colf = perm_row(j);
-      const int col = gemm_col0(g, kt) + colf;
-      const bool cok = colf < gemm_col_valid(g, kt);
+    for (int t = 0; t < 8; ++t) dw_flush<P_FW>(a.grad, wave, 256, 32 * t, 32, acc[t], lane);
+    dw_flush_bias<P_FB>(a.grad, wave, 256, dbias, lane);
+    dw_flush<P_AW>(a.grad, 0, 1, 32 * wave, 32, acc2, lane);
+    if (wave == 0) dw_flush_bias<P_AB>(a.grad, 0, 1, dbias2, lane);
+  } else {
+    if (!vr_rgb) {
 #pragma unroll
-      for (int rho = 0; rho < 16; ++rho) {
-        const int n = 32 * (nt0 + wave) + perm_row(acc_row(rho, h));
-        if (cok && n < nvalid) atomicAdd(gw + (int64_t)n * K + col, acc[t][rho]);
-      }
+      for (int t = 0; t < 9; ++t) dw_flush<P_VW>(a.grad, wave, 128, 32 * t, t < 8 ? 32 : 27, acc[t], lane);
+      dw_flush_bias<P_VB>(a.grad, wave, 128, dbias, lane);
+    } else {
+      dw_flush<P_RW>(a.grad, 0, 3, 32 * (wave - 4), 32, acc[0], lane);
+      if (wave == 4) dw_flush_bias<P_RB>(a.grad, 0, 3, dbias, lane);
     }
   }
-  if (job.kg == 0) {
-    dbias += __shfl_xor(dbias, 32, 64);
-    const int n = 32 * (nt0 + wave) + perm_row(j);
-    if (h == 0 && n < nvalid) atomicAdd(a.grad + param_offset(wp + 1) + n, dbias);
+}
+
+template <class P>
+__global__ void __launch_bounds__(DW_WAVES * 64) dw_kernel(DwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
+  char* lds = (char*)smem_u4;
+  const int item = blockIdx.x;
+  int j = 0;
+#pragma unroll
+  for (int k = 1; k < NDWJOB; ++k) j += a.item_off[k] <= item ? 1 : 0;
+  const int n_items = a.item_off[j + 1] - a.item_off[j], i = item - a.item_off[j];
+  const int64_t b_begin = a.nblk * i / n_items, b_end = a.nblk * (i + 1) / n_items;
+  switch (j) {
+    case 0: dw_job<P, 0>(a, b_begin, b_end, lds); break;
+    case 1: dw_job<P, 1>(a, b_begin, b_end, lds); break;
+    case 2: dw_job<P, 2>(a, b_begin, b_end, lds); break;
+    case 3: dw_job<P, 3>(a, b_begin, b_end, lds); break;
+    case 4: dw_job<P, 4>(a, b_begin, b_end, lds); break;
+    case 5: dw_job<P, 5>(a, b_begin, b_end, lds); break;
+    case 6: dw_job<P, 6>(a, b_begin, b_end, lds); break;
+    case 7: dw_job<P, 7>(a, b_begin, b_end, lds); break;
+    case 8: dw_job<P, 8>(a, b_begin, b_end, lds); break;
+    default: dw_job<P, 9>(a, b_begin, b_end, lds); break;
   }
 }
 
@@ -1036,12 +1147,31 @@ int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const floa
   return check_launch("nerf_mlp_fwd");
 }
 
-int64_t nerf_mlp_dw_chunk(int64_t M) {
-  // samples per dW job (multiple of 256): >= 8 chunks so every CU gets work, <= 16384
-  const int64_t ldm = nerf_mlp_padded_samples(M);
-  int64_t ch = 16384;
-  while (ch > 256 && ldm / ch < 8) ch /= 2;
-  return ch;
+// work items of the dW launch: at most one per CU (a single wave of workgroups that ends
+// together), split across the 10 jobs in proportion to the bytes each reads, at least one
+// and at most one per block per job
+static int cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess || n <= 0)
+    n = 256;
+  return n;
+}
+static void dw_items(int64_t nblk, int item_off[NDWJOB + 1]) {
+  static const int target = cu_count();
+  int tiles = 0;
+  for (int j = 0; j < NDWJOB; ++j) tiles += dw_job_tiles(j);
+  item_off[0] = 0;
+  for (int j = 0; j < NDWJOB; ++j) {
+    int64_t n = target * (int64_t)dw_job_tiles(j) / tiles;
+    n = n < 1 ? 1 : n > nblk ? nblk : n;
+    item_off[j + 1] = item_off[j] + (int)n;
+  }
+}
+int64_t nerf_mlp_dw_items(int64_t M) {
+  int off[NDWJOB + 1];
+  dw_items(nerf_mlp_padded_samples(M) / 32, off);
+  return off[NDWJOB];
 }
 
 // dX chain only: dz (per-layer output gradients, fragment-native tiles) from d_raw + masks
@@ -1065,10 +1195,9 @@ int nerf_mlp_bwd_dw(int dtype, int64_t M, const void* act, const void* dz, float
   if (M == 0) return 0;
   NERF_REQUIRE(act && dz && grad, "nerf_mlp_bwd_dw: null pointer");
   const int64_t nblk = nerf_mlp_padded_samples(M) / 32;
-  const int64_t chunk_blk = nerf_mlp_dw_chunk(M) / 32;
-  const int nchunks = (int)((nblk + chunk_blk - 1) / chunk_blk);
-  DwArgs w{dz, act, nblk, chunk_blk, nchunks, grad};
-  dim3 grid((unsigned)(n_dw_jobs_per_chunk() * nchunks));
+  DwArgs w{dz, act, nblk, grad, {}};
+  dw_items(nblk, w.item_off);
+  dim3 grid((unsigned)w.item_off[NDWJOB]);
   if (dtype == 0) {
     allow_lds(dw_kernel<PF32>, dw_lds_bytes<PF32>());
     hipLaunchKernelGGL((dw_kernel<PF32>), grid, dim3(DW_WAVES * 64), dw_lds_bytes<PF32>(), stream, w);

@@ -1,0 +1,68 @@
+"""Static checks on the gfx950 assembly of the MLP kernels (hipcc --save-temps):
+  * the forward / dX kernels are straight-line (no loop: a runtime walk of the constexpr
+    layout tables would show up as one),
+  * every counted `s_waitcnt vmcnt(N)` + s_barrier hand-off waits for the weight DMA:
+    N <= vector-memory ops issued after the last global_load_lds before it,
+  * no scratch (spills).
+    python tools/asm_check.py            (exit status 1 on a violation)
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = ["fwd_kernel<nerf::mlp::PBF16, true, false>", "fwd_kernel<nerf::mlp::PBF16, false, false>",
+           "fwd_kernel<nerf::mlp::PBF16, false, true>", "fwd_kernel<nerf::mlp::PF32, true, false>",
+           "fwd_kernel<nerf::mlp::PF32, false, false>", "dx_kernel<nerf::mlp::PBF16>", "dx_kernel<nerf::mlp::PF32>",
+           "dw_kernel<nerf::mlp::PBF16>", "dw_kernel<nerf::mlp::PF32>"]
+
+
+def build_asm(tmp):
+    src = os.path.join(tmp, "k.hip")
+    args = {"fwd": "(nerf::mlp::FwdArgs)", "dx_": "(nerf::mlp::DxArgs)", "dw_": "(nerf::mlp::DwArgs)"}
+    with open(src, "w") as f:
+        f.write("#define NERF_MLP_DEVICE_ONLY\n")
+        f.write(f'#include "{ROOT}/nerf-replication_amd/csrc/mlp.hip"\n')
+        for k in KERNELS:
+            f.write(f"template __global__ void nerf::mlp::{k}{args[k[:3]]};\n")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include",
+                    "--cuda-device-only", "-S", src, "-o", os.path.join(tmp, "k.s")], check=True, cwd=tmp)
+    return open(os.path.join(tmp, "k.s")).read()
+
+
+def check(asm):
+    bad = 0
+    for name in re.findall(r"^(_Z\w+):", asm, re.M):
+        body = asm[asm.index(name + ":"):]
+        body = body[:body.index("s_endpgm")]
+        lines = body.splitlines()
+        labels = {m.group(1): i for i, l in enumerate(lines) for m in [re.match(r"^(\.LBB\w+):", l)] if m}
+        loops = [i for i, l in enumerate(lines) for m in [re.search(r"s_(?:cbranch_\w+|branch)\s+(\.LBB\w+)", l)]
+                 if m and m.group(1) in labels and labels[m.group(1)] < i]
+        since, waits, unsafe = None, 0, 0
+        for i, l in enumerate(lines):
+            t = l.strip()
+            if t.startswith("global_load_lds"):
+                since = 0
+            elif since is not None and re.match(r"(global_store|global_load|scratch_|buffer_|global_atomic)", t):
+                since += 1
+            m = re.match(r"s_waitcnt vmcnt\((\d+)\)", t)
+            if m and i + 1 < len(lines) and "s_barrier" in lines[i + 1] and since is not None:
+                waits += 1
+                unsafe += int(m.group(1)) > since
+        straight = "dw_kernel" in name or not loops
+        ok = straight and not unsafe
+        bad += not ok
+        print(f"{'ok ' if ok else 'BAD'} {name[:70]:70s} loops={len(loops)} counted_waits={waits} unsafe={unsafe}")
+    for m in re.finditer(r"\.name:\s+(\S+)\n(?:.*\n){0,40}?\s+\.private_segment_fixed_size:\s+(\d+)", asm):
+        if int(m.group(2)):
+            bad += 1
+            print(f"BAD scratch {m.group(2)} B in {m.group(1)}")
+    return bad
+
+
+if __name__ == "__main__":
+    with tempfile.TemporaryDirectory() as tmp:
+        sys.exit(1 if check(build_asm(tmp)) else 0)
