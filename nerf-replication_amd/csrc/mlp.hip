@@ -844,13 +844,27 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
 typedef __attribute__((ext_vector_type(4))) short short4_t;
 typedef __attribute__((address_space(3))) short4_t lds_short4;
 
+// bf16 LDS swizzle of the dW ring.  A stored chunk is 64 lane-linear 16-B pieces; the
+// transposed fragment read below touches pieces p = 16 a + b with b in {q, q + 4} (+ 8 for
+// lanes 32..63), a in {s, s + 2}, of both chunks of a tile at once -- 16 of the 64 banks
+// as stored.  Piece p of chunk c is placed at slot 16 a + (b + 4 (a >> 1) + 8 c) mod 16
+// instead (the DMA's per-lane source address does the permutation for free), which makes
+// every ds_read_b64_tr_b16 conflict-free.
+__host__ __device__ constexpr int dw_swz(int c, int p) {
+  return 16 * (p >> 4) + (((p & 15) + 4 * ((p >> 4) >> 1) + 8 * c) & 15);
+}
+__host__ __device__ constexpr int dw_unswz(int c, int slot) {
+  return 16 * (slot >> 4) + (((slot & 15) - 4 * ((slot >> 4) >> 1) - 8 * c) & 15);
+}
+
 // bf16: the 8-sample K fragment (samples 16 s + 8 h + [0, 8)) of row (lane & 31)
 __device__ __forceinline__ bf16x8 dw_frag_bf16(const char* tile, int s, int lane) {
   const int l16 = lane & 15, G = lane >> 4;
   const int hp = G & 1, h = G >> 1, q = l16 >> 2, pp = l16 & 3;
-  const char* base = tile + (pp >> 1) * 1024 + (pp & 1) * 8 + (16 * s + 8 * h + q + 32 * hp) * 16;
-  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)base);
-  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(base + 4 * 16));
+  const int c = pp >> 1, p = 16 * s + 8 * h + q + 32 * hp;
+  const char* base = tile + c * 1024 + (pp & 1) * 8;
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(base + dw_swz(c, p) * 16));
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(base + dw_swz(c, p + 4) * 16));
   typedef __attribute__((ext_vector_type(8))) short short8_t;
   short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, v);
@@ -934,7 +948,8 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
     for (int q = 0; q < NT; ++q)
       if (q == slot) tau = q < JD.nd ? JD.dz[q] : JD.act[q - JD.nd];
     const int ntiles = is_dz ? ZT_TILES : AT_TILES;
-    src[i] = (const char*)(is_dz ? a.dz : a.act) + tile_kib(a.nblk, ntiles, tau, 0, c, P::CH) * 1024 + lane * 16;
+    const int piece = P::CH == 2 ? dw_unswz(c, lane) : lane;  // bf16 ring is swizzled (dw_swz)
+    src[i] = (const char*)(is_dz ? a.dz : a.act) + tile_kib(a.nblk, ntiles, tau, 0, c, P::CH) * 1024 + piece * 16;
     bstride[i] = block_stride_kib(ntiles, P::CH) * 1024;
     dst[i] = (uint32_t)(slot * TB + c * 1024);
   }
