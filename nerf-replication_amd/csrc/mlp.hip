@@ -280,19 +280,6 @@ struct GroupTable {
   static constexpr Groups<DIR, DENSITY, CH> t{};
 };
 
-// issue the DMA of group G into slot `slot`: every wave issues exactly NF wave-instructions
-// (the last chunk is re-copied by the surplus waves -- identical bytes), so the count a
-// later wait needs is a compile-time constant.
-template <class P, int C0, int NCH>
-__device__ __forceinline__ void fetch_group(const uint4* gsrc, uint32_t slot_base, int wave, int lane) {
-  constexpr int NF = (NCH + P::WAVES - 1) / P::WAVES;
-#pragma unroll
-  for (int i = 0; i < NF; ++i) {
-    const int k = cmin(wave + P::WAVES * i, NCH - 1);
-    glds16_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
-  }
-}
-
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const u32x4 lds_cu4;
 __device__ __forceinline__ uint4 as_uint4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
@@ -306,15 +293,122 @@ __device__ __forceinline__ lds_cu4* lds_ptr(uint32_t byte_addr) {
   return (lds_cu4*)(uintptr_t)byte_addr;
 }
 
-template <class P>
-__device__ __forceinline__ f32x16 tile_mma(lds_cu4* unit_lane, int tile_idx, const typename P::Tile& b, f32x16 acc) {
-#pragma unroll
-  for (int c = 0; c < P::CH; ++c) {
-    const uint4 a = as_uint4(unit_lane[(tile_idx * P::CH + c) * 64]);
-    acc = P::mma(a, b, c, acc);
-  }
-  return acc;
+// The MFMA steps of a group as one flat compile-time list: step k = (unit j of the group,
+// input tile t, chunk c), in execution order.  A group's body is straight-line code over
+// it with the A operand (weights, LDS) prefetched PD steps ahead across unit boundaries
+// -- hipcc on its own keeps one ds_read in flight and waits lgkmcnt(0) before every MFMA.
+struct Step { int j, u, t, c, off, kin, len; bool first, last; };
+template <int DIR> __host__ __device__ constexpr int unit_tiles(int u) {
+  return DIR == 0 ? fwd_unit_tiles(u) : bwd_unit_tiles(u);
 }
+template <int DIR, bool DENSITY, int CH>
+__host__ __device__ constexpr int group_steps(int g) {
+  const Group G = GroupTable<DIR, DENSITY, CH>::t.g[g];
+  int n = 0;
+  for (int j = 0; j < G.n; ++j) n += unit_tiles<DIR>(G.u0 + j) * CH;
+  return n;
+}
+template <int DIR, bool DENSITY, int CH>
+__host__ __device__ constexpr Step group_step(int g, int k) {
+  const Group G = GroupTable<DIR, DENSITY, CH>::t.g[g];
+  for (int j = 0; j < G.n; ++j) {
+    const int u = G.u0 + j, n = unit_tiles<DIR>(u) * CH;
+    if (k < n) {
+      const int t = k / CH, c = k % CH;
+      return Step{j, u, t, c, unit_chunk_off<DIR>(u, CH) - G.c0 + k, k, n, k == 0, k == n - 1};
+    }
+    k -= n;
+  }
+  return Step{-1, -1, 0, 0, 0, 0, 0, false, false};
+}
+// A-operand prefetch distance in steps (a bf16 step is one 32-cycle MFMA, an fp32 step four
+// 64-cycle ones) and how many steps into unit j + 1 the finish of unit j is issued (its
+// VALU then interleaves with unit j + 1's MFMAs instead of stalling the wave)
+#ifndef NERF_PREFETCH_BF16
+#define NERF_PREFETCH_BF16 3
+#endif
+#ifndef NERF_FINISH_DELAY
+#define NERF_FINISH_DELAY 3
+#endif
+template <class P> __host__ __device__ constexpr int prefetch_depth() { return P::CH == 2 ? NERF_PREFETCH_BF16 : 2; }
+constexpr int FINISH_DELAY = NERF_FINISH_DELAY;
+
+// W: the wave object; it provides in_tile<u, t>(), prefetch<u>() (issue unit u's side
+// reads one unit ahead), init<u>(acc) (initial accumulator) and finish<u>(acc)
+#ifndef NERF_CROSS_GROUP_FINISH
+#define NERF_CROSS_GROUP_FINISH 1
+#endif
+// the unit finished inside group g: (first, last] = units whose finish is issued in g.
+// With CROSS_GROUP_FINISH the last unit of a group is finished FINISH_DELAY steps into the
+// next group (after the barrier), so no group ends in a VALU burst that every wave of the
+// workgroup runs at once; its stores then count against the next group's hand-off.
+template <int DIR, bool DENSITY, int CH>
+__host__ __device__ constexpr bool finished_in_group(int g, int u) {
+  const auto& T = GroupTable<DIR, DENSITY, CH>::t;
+  const Group G = T.g[g];
+  const int last = G.u0 + G.n - 1;
+  if (!NERF_CROSS_GROUP_FINISH) return u >= G.u0 && u <= last;
+  const bool prev = g > 0 && u == T.g[g - 1].u0 + T.g[g - 1].n - 1;
+  return prev || (u >= G.u0 && (u < last || (u == last && g + 1 == T.n)));
+}
+
+// W: the wave object; it provides in_tile<u, t>(), prefetch<u>() (issue unit u's side
+// reads one unit ahead), init<u>(acc) (initial accumulator), finish<u>(acc) and a
+// pending accumulator `pend` that carries a finished chain to its deferred finish
+template <class P, int DIR, bool DENSITY, int g, class W>
+__device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
+  constexpr int NS = group_steps<DIR, DENSITY, P::CH>(g);
+  constexpr int PDP = prefetch_depth<P>();
+  constexpr auto& T = GroupTable<DIR, DENSITY, P::CH>::t;
+  constexpr Group G = T.g[g];
+  constexpr bool LASTG = g + 1 == T.n;
+  constexpr int PREV_U = g > 0 ? T.g[g - 1].u0 + T.g[g - 1].n - 1 : -1;  // previous group's last unit
+  uint4 ring[PDP];
+  sfor<(NS < PDP ? NS : PDP)>([&](auto kk) {
+    constexpr int k = decltype(kk)::value;
+    constexpr Step S = group_step<DIR, DENSITY, P::CH>(g, k);
+    ring[k] = as_uint4(wl[S.off * 64]);
+  });
+  w.template prefetch<G.u0>();
+  f32x16 acc;
+  sfor<NS>([&](auto kk) {
+    constexpr int k = decltype(kk)::value;
+    constexpr Step S = group_step<DIR, DENSITY, P::CH>(g, k);
+    const uint4 a = ring[k % PDP];
+    if constexpr (k + PDP < NS) {
+      constexpr Step N = group_step<DIR, DENSITY, P::CH>(g, k + PDP);
+      ring[k % PDP] = as_uint4(wl[N.off * 64]);
+    }
+    if constexpr (S.first) {
+      if constexpr (S.j > 0) w.pend = acc;
+      w.template init<S.u>(acc);
+      if constexpr (S.j + 1 < G.n) w.template prefetch<S.u + 1>();
+    }
+    acc = P::mma(a, w.template in_tile<S.u, S.t>(), S.c, acc);
+    constexpr int U_BEFORE = S.j > 0 ? S.u - 1 : PREV_U;
+    if constexpr (U_BEFORE >= 0 && finished_in_group<DIR, DENSITY, P::CH>(g, U_BEFORE) &&
+                  S.kin == (FINISH_DELAY < S.len - 1 ? FINISH_DELAY : S.len - 1))
+      w.template finish<U_BEFORE>(w.pend);
+    if constexpr (S.last && S.j == G.n - 1) {
+      if constexpr (finished_in_group<DIR, DENSITY, P::CH>(g, S.u)) w.template finish<S.u>(acc);
+      else w.pend = acc;
+    }
+  });
+}
+
+// issue the DMA of group G into slot `slot`: every wave issues exactly NF wave-instructions
+// (the last chunk is re-copied by the surplus waves -- identical bytes), so the count a
+// later wait needs is a compile-time constant.
+template <class P, int C0, int NCH>
+__device__ __forceinline__ void fetch_group(const uint4* gsrc, uint32_t slot_base, int wave, int lane) {
+  constexpr int NF = (NCH + P::WAVES - 1) / P::WAVES;
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int k = cmin(wave + P::WAVES * i, NCH - 1);
+    glds16_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
+  }
+}
+
 
 // ------------------------------------------------------------------------------------
 // positional encoding straight into accumulator-layout tiles
@@ -406,20 +500,6 @@ __device__ __forceinline__ void store_tile(void* base, int64_t nblk, int ntiles,
   for (int c = 0; c < P::CH; ++c) dst[c * 64] = P::chunk(t, c);
 }
 
-// bias chunk of a unit: lanes 0..7 hold its 32 fp32 biases; rows 8q + 4h + {0..3} =
-// lane (2q + h).  `half` points at lane h of the chunk.
-__device__ __forceinline__ f32x16 bias_init(lds_cu4* half) {
-  f32x16 acc;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint4 b = as_uint4(half[2 * q]);
-    acc[4 * q + 0] = __uint_as_float(b.x);
-    acc[4 * q + 1] = __uint_as_float(b.y);
-    acc[4 * q + 2] = __uint_as_float(b.z);
-    acc[4 * q + 3] = __uint_as_float(b.w);
-  }
-  return acc;
-}
 
 // ReLU masks of the training forward, read by the dX chain: per 32-sample wave block,
 // MASK_GROUPS x 64 lanes x 16 B; group l < 8 = layer l's 8 output tiles (tile n -> dword
@@ -462,6 +542,9 @@ struct FwdWave {
   Tile X[2], D, Ha[8], Hb[8];
   uint32_t mw[4];
   float alpha, rgb0, rgb1, rgb2;
+  lds_cu4* wb;      // current group's slot + 16 h (bias reads)
+  uint4 bias[4];
+  f32x16 pend;      // finished accumulator awaiting its deferred finish (group_body)
 
   __device__ __forceinline__ FwdWave(const FwdArgs& args, const uint4* smem) : a(args), lds(smem) {
     gw = (const uint4*)a.wpack;
@@ -479,7 +562,7 @@ struct FwdWave {
   }
 
   // input tile t of layer L (mlp_tables.h: Ha/Hb ping-pong, PE tiles X / D)
-  template <int L, int t> __device__ __forceinline__ const Tile& in_tile() const {
+  template <int L, int t> __device__ __forceinline__ const Tile& in_tile_L() const {
     if constexpr (L == L0) return X[t];
     else if constexpr (L == L5) { if constexpr (t < 2) return X[t]; else return Ha[t - 2]; }
     else if constexpr (L == LV) { if constexpr (t < 8) return Ha[t]; else return D; }
@@ -502,19 +585,22 @@ struct FwdWave {
   }
   static __host__ __device__ constexpr int group_stores(int g) {
     int s = 0;
-    for (int j = 0; j < GT::t.g[g].n; ++j) s += unit_stores(GT::t.g[g].u0 + j);
+    for (int u = 0; u < NUNIT_FWD; ++u)
+      if (finished_in_group<0, DENSITY, P::CH>(g, u)) s += unit_stores(u);
     return s;
   }
 
-  template <int L, int n> __device__ __forceinline__ void finish(const f32x16& acc) {
+  template <int L, int n> __device__ __forceinline__ void finish_L(const f32x16& acc) {
     if constexpr (L <= L7 || L == LV) {
       Tile out;
       uint32_t bits = 0;
 #pragma unroll
       for (int rho = 0; rho < 16; ++rho) {
-        const float x = acc[rho];
-        bits |= (x > 0.f ? 1u : 0u) << rho;
-        P::set(out, rho, x > 0.f ? x : 0.f);
+        // ReLU as an integer max on the float bits (negative floats are negative ints): one
+        // v_max_i32, no NaN canonicalisation; mask bit = (x > 0) = min(relu bits, 1)
+        const int y = max(__float_as_int(acc[rho]), 0);
+        if constexpr (STORE) bits |= min((uint32_t)y, 1u) << rho;
+        P::set(out, rho, __int_as_float(y));
       }
       out_arr<L>()[n] = out;
       if constexpr (STORE) {
@@ -542,9 +628,25 @@ struct FwdWave {
     }
   }
 
-  template <int u> __device__ __forceinline__ void unit(uint32_t unit_addr) {
+  // ---- group_body hooks
+  template <int u> static __host__ __device__ constexpr int group_of() {
+    int g = 0;
+    while (!(GT::t.g[g].u0 <= u && u < GT::t.g[g].u0 + GT::t.g[g].n)) ++g;
+    return g;
+  }
+  template <int u, int t> __device__ __forceinline__ const Tile& in_tile() const {
+    return in_tile_L<fwd_unit_layer(u), t>();
+  }
+  // the unit's bias chunk (rows 8q + 4h + {0..3} = lane 2q + h) is the MFMA chain's
+  // initial accumulator; it is read one unit ahead
+  template <int u> __device__ __forceinline__ void prefetch() {
+    constexpr int L = fwd_unit_layer(u);
+    constexpr int BOFF = unit_chunk_off<0>(u, CH) - GT::t.g[group_of<u>()].c0 + fwd_in_tiles(L) * CH;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bias[q] = as_uint4(wb[BOFF * 64 + 2 * q]);
+  }
+  template <int u> __device__ __forceinline__ void init(f32x16& acc) {
     constexpr int L = fwd_unit_layer(u), n = u - fwd_unit_first(L);
-    constexpr int T = fwd_in_tiles(L);
     if constexpr (L == L5 && n == 0) {  // PE recomputed for the skip instead of held through L1..L4
       settle(px);  // opaque to hipcc: it would otherwise CSE this with the L0 tiles and hold them
       settle(py);
@@ -558,27 +660,25 @@ struct FwdWave {
       settle(dz);
       pe_tile<P, 0, 4, 27>(D, h, dx, dy, dz);
     }
-    f32x16 acc = bias_init(lds_ptr(unit_addr + (uint32_t)(T * CH * 1024 + h * 16)));
-    lds_cu4* w = lds_ptr(unit_addr + (uint32_t)(lane * 16));
-    sfor<T>([&](auto tt) {
-      constexpr int t = decltype(tt)::value;
-      acc = tile_mma<P>(w, t, in_tile<L, t>(), acc);
-    });
-    finish<L, n>(acc);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc[4 * q + 0] = __uint_as_float(bias[q].x);
+      acc[4 * q + 1] = __uint_as_float(bias[q].y);
+      acc[4 * q + 2] = __uint_as_float(bias[q].z);
+      acc[4 * q + 3] = __uint_as_float(bias[q].w);
+    }
+  }
+  template <int u> __device__ __forceinline__ void finish(const f32x16& acc) {
+    constexpr int L = fwd_unit_layer(u), n = u - fwd_unit_first(L);
+    finish_L<L, n>(acc);
   }
 
   template <int g> __device__ __forceinline__ void step() {
-    constexpr Group G = GT::t.g[g];
     constexpr int NG = GT::t.n;
     if constexpr (g + 1 < NG) fetch<g + 1>();
-    sfor<G.n>([&](auto jj) {
-      constexpr int u = G.u0 + decltype(jj)::value;
-      constexpr int off = (g % NSLOT) * SLOT_CAP + unit_chunk_off<0>(u, CH) - G.c0;  // compile time
-      unit<u>(lds_base + (uint32_t)(off * 1024));
-      // one scheduling region per unit: hipcc would otherwise hoist every LDS read of the
-      // group (up to 256 VGPRs of A operands) to its top and spill
-      __builtin_amdgcn_sched_barrier(0);
-    });
+    const uint32_t slot = lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024);
+    wb = lds_ptr(slot + (uint32_t)(h * 16));
+    group_body<P, 0, DENSITY, g>(*this, lds_ptr(slot + (uint32_t)(lane * 16)));
     if constexpr (g + 1 < NG) wait_barrier<group_stores(g)>();
   }
 
@@ -648,6 +748,7 @@ struct DxWave {
   int64_t wblock, m;
   Tile G, DA, Ha[8], Hb[8];
   uint4 mk[MASK_GROUPS];
+  f32x16 pend;      // finished accumulator awaiting its deferred finish (group_body)
 
   __device__ __forceinline__ DxWave(const DxArgs& args, const uint4* smem) : a(args), lds(smem) {
     gw = (const uint4*)a.wpack_t;
@@ -664,7 +765,7 @@ struct DxWave {
     fetch_group<P, Gr.c0, Gr.nch>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
   }
 
-  template <int s, int t> __device__ __forceinline__ const Tile& in_tile() const {
+  template <int s, int t> __device__ __forceinline__ const Tile& in_tile_S() const {
     if constexpr (s == B_RGB) return G;
     else if constexpr (s == B_V) return Hb[t];
     else if constexpr (s == B_FA) { if constexpr (t < 8) return Ha[t]; else return DA; }
@@ -682,19 +783,24 @@ struct DxWave {
   static __host__ __device__ constexpr int mask_group(int s) {
     return s == B_RGB ? 8 : s == B_V ? -1 : s == B_FA ? 7 : bwd_fwd_layer(s) - 1;
   }
-  static __host__ __device__ constexpr int group_stores(int g) { return GT::t.g[g].n * CH; }
+  static __host__ __device__ constexpr int group_stores(int g) {
+    int s = 0;
+    for (int u = 0; u < NUNIT_BWD; ++u)
+      if (finished_in_group<1, false, P::CH>(g, u)) s += CH;
+    return s;
+  }
 
-  template <int u> __device__ __forceinline__ void unit(uint32_t unit_addr) {
-    constexpr int s = bwd_unit_stage(u), j = u - bwd_unit_first(s);
-    constexpr int T = bwd_in_tiles(s);
-    f32x16 acc;
+  // ---- group_body hooks
+  template <int u, int t> __device__ __forceinline__ const Tile& in_tile() const {
+    return in_tile_S<bwd_unit_stage(u), t>();
+  }
+  template <int u> __device__ __forceinline__ void prefetch() {}
+  template <int u> __device__ __forceinline__ void init(f32x16& acc) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    lds_cu4* w = lds_ptr(unit_addr + (uint32_t)(lane * 16));
-    sfor<T>([&](auto tt) {
-      constexpr int t = decltype(tt)::value;
-      acc = tile_mma<P>(w, t, in_tile<s, t>(), acc);
-    });
+  }
+  template <int u> __device__ __forceinline__ void finish(const f32x16& acc) {
+    constexpr int s = bwd_unit_stage(u), j = u - bwd_unit_first(s);
     constexpr int mg = mask_group(s);
     uint32_t mask = 0xFFFFu;
     if constexpr (mg >= 0) {
@@ -710,15 +816,10 @@ struct DxWave {
   }
 
   template <int g> __device__ __forceinline__ void step() {
-    constexpr Group Gr = GT::t.g[g];
     constexpr int NG = GT::t.n;
     if constexpr (g + 1 < NG) fetch<g + 1>();
-    sfor<Gr.n>([&](auto jj) {
-      constexpr int u = Gr.u0 + decltype(jj)::value;
-      constexpr int off = (g % NSLOT) * SLOT_CAP + unit_chunk_off<1>(u, CH) - Gr.c0;  // compile time
-      unit<u>(lds_base + (uint32_t)(off * 1024));
-      __builtin_amdgcn_sched_barrier(0);
-    });
+    const uint32_t slot = lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024);
+    group_body<P, 1, false, g>(*this, lds_ptr(slot + (uint32_t)(lane * 16)));
     if constexpr (g + 1 < NG) wait_barrier<group_stores(g)>();
   }
 

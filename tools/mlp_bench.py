@@ -28,9 +28,13 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--lib", default=None, help="alternative build of libnerf_amd.so (kernel experiments)")
+    ap.add_argument("--libs", default=None, help="comma-separated builds, timed in interleaved rounds in this process")
+    ap.add_argument("--rounds", type=int, default=5)
     args = ap.parse_args()
     if args.lib:
         _lib.LIB_PATH = os.path.abspath(args.lib)
+    if args.libs:
+        return compare(args)
     dev = torch.device("cuda:0")
     dt = ops.dtype_code(args.dtype)
     torch.manual_seed(0)
@@ -85,6 +89,76 @@ def main():
         if name in FLOP:
             ent["tflops"] = round(FLOP[name] * M / (ms * 1e-3) / 1e12, 1)
         out[name] = ent
+    print(json.dumps(out), flush=True)
+
+
+def load_handle(path):
+    import ctypes
+    h = ctypes.CDLL(os.path.abspath(path))
+    for name, (res, argt) in _lib.SIGNATURES.items():
+        fn = getattr(h, name)
+        fn.restype = res
+        fn.argtypes = argt
+    return h
+
+
+def compare(args):
+    """Interleaved rounds over several builds in one process (cross-process variance and
+    DVFS drift otherwise look like kernel differences): median ms per kernel per build."""
+    import statistics
+    dev = torch.device("cuda:0")
+    dt = ops.dtype_code(args.dtype)
+    M = args.M
+    torch.manual_seed(0)
+    shapes = [(256, 63), (256,)] + [(256, 256), (256,)] * 4 + [(256, 319), (256,)] + [(256, 256), (256,)] * 2 + \
+             [(128, 283), (128,), (256, 256), (256,), (1, 256), (1,), (3, 128), (3,)]
+    params = [(torch.rand(s, device=dev) - 0.5) * (0.2 if len(s) == 2 else 0.1) for s in shapes]
+    import ctypes
+    arr = ctypes.cast((ctypes.c_void_p * 24)(*[p.data_ptr() for p in params]), ctypes.c_void_p)
+    pts = (torch.rand(M, 3, device=dev) - 0.5) * 3
+    vd = torch.nn.functional.normalize(torch.randn(M // 192 + 1, 3, device=dev), dim=-1)
+    d_raw = torch.randn(M, 4, device=dev) * 1e-3
+    s = torch.cuda.current_stream().cuda_stream
+    libs = [(os.path.basename(p).replace(".so", ""), load_handle(p)) for p in args.libs.split(",")]
+    bufs = {}
+    for name, L in libs:
+        pf = torch.empty(L.nerf_mlp_packed_bytes(dt, 0), dtype=torch.uint8, device=dev)
+        pb = torch.empty(L.nerf_mlp_packed_bytes(dt, 1), dtype=torch.uint8, device=dev)
+        L.nerf_mlp_pack(arr, dt, ptr(pf), ptr(pb), s)
+        bufs[name] = dict(pf=pf, pb=pb, raw=torch.empty(M, 4, device=dev),
+                          act=torch.empty(L.nerf_mlp_act_bytes(dt, M), dtype=torch.uint8, device=dev),
+                          masks=torch.empty(L.nerf_mlp_mask_bytes(M), dtype=torch.uint8, device=dev),
+                          dz=torch.empty(L.nerf_mlp_dz_bytes(dt, M), dtype=torch.uint8, device=dev),
+                          grad=torch.zeros(L.nerf_mlp_net_params(), device=dev))
+
+    def kernels(L, b):
+        return {
+            "fwd": lambda: L.nerf_mlp_fwd(ptr(b["pf"]), dt, ptr(pts), ptr(vd), 192, None, M, 0, ptr(b["raw"]), None,
+                                          None, s),
+            "fwd_train": lambda: L.nerf_mlp_fwd(ptr(b["pf"]), dt, ptr(pts), ptr(vd), 192, None, M, 1, ptr(b["raw"]),
+                                                ptr(b["act"]), ptr(b["masks"]), s),
+            "dx": lambda: L.nerf_mlp_bwd_dx(ptr(b["pb"]), dt, ptr(d_raw), M, ptr(b["masks"]), ptr(b["dz"]), s),
+            "dw": lambda: L.nerf_mlp_bwd_dw(dt, M, ptr(b["act"]), ptr(b["dz"]), ptr(b["grad"]), s),
+        }
+    times = {(n, k): [] for n, _ in libs for k in ("fwd", "fwd_train", "dx", "dw")}
+    for r in range(args.rounds + 1):
+        for name, L in libs:
+            for k, fn in kernels(L, bufs[name]).items():
+                fn()
+                torch.cuda.synchronize()
+                a = torch.cuda.Event(enable_timing=True)
+                e = torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(args.reps):
+                    st = fn()
+                    assert st == 0, (name, k)
+                e.record()
+                torch.cuda.synchronize()
+                if r:
+                    times[(name, k)].append(a.elapsed_time(e) / args.reps)
+    out = {"M": M, "rounds": args.rounds}
+    for name, _ in libs:
+        out[name] = {k: round(statistics.median(times[(name, k)]), 4) for k in ("fwd", "fwd_train", "dx", "dw")}
     print(json.dumps(out), flush=True)
 
 
