@@ -98,8 +98,9 @@ def build(args, device):
 
 def train_step(cfg, trainer, opt, ds, device):
     rays, rgbs = ds.sample_batch()
-    batch = {"rays": rays[None], "rgbs": rgbs[None], "near": torch.tensor([2.0], device=device),
-             "far": torch.tensor([6.0], device=device)}
+    from nerf_amd import ops
+    batch = {"rays": rays[None], "rgbs": rgbs[None], "near": ops.device_scalar(2.0, device),
+             "far": ops.device_scalar(6.0, device)}
     return trainer.train_step(batch, opt)
 
 

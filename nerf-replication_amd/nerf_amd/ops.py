@@ -62,10 +62,26 @@ def device_table(kind: str, a: float, b: float, n_or_step, device) -> torch.Tens
     return t
 
 
+_dev_scalars = {}
+
+
+def device_scalar(x: float, device) -> torch.Tensor:
+    """A cached 1-element fp32 device tensor.  Building one per call (torch.tensor(...,
+    device=)) is a pageable host-to-device copy, which blocks the host until the GPU queue
+    has drained: at every training step that idles the GPU for the whole Python launch
+    sequence."""
+    key = (float(x), str(torch.device(device)))
+    t = _dev_scalars.get(key)
+    if t is None:
+        t = torch.tensor([float(x)], dtype=torch.float32, device=device)
+        _dev_scalars[key] = t
+    return t
+
+
 def _scalar_dev(x, device) -> torch.Tensor:
     if isinstance(x, torch.Tensor):
         return x.reshape(-1)[:1].to(device=device, dtype=torch.float32).contiguous()
-    return torch.tensor([float(x)], dtype=torch.float32, device=device)
+    return device_scalar(x, device)
 
 
 # --------------------------------------------------------------------------------------
@@ -233,6 +249,7 @@ class _Composite(torch.autograd.Function):
         w = torch.empty(R, S, device=dev, dtype=torch.float32)
         check(lib().nerf_composite_fwd(ptr(raw), ptr(z), dptr, dstride, R, S, int(bool(white)), ptr(rgb), ptr(depth),
                                        ptr(acc), ptr(w), stream_of(raw)), "nerf_composite_fwd")
+        ctx.set_materialize_grads(False)  # unused outputs (depth, acc) arrive as None, not zero-filled
         ctx.save_for_backward(raw, z, keep)
         ctx.dptr, ctx.dstride, ctx.white = dptr, dstride, int(bool(white))
         ctx.mark_non_differentiable(w)
@@ -240,6 +257,8 @@ class _Composite(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_rgb, g_depth, g_acc, g_w):
+        if g_rgb is None and g_depth is None and g_acc is None:
+            return None, None, None, None
         raw, z, _keep = ctx.saved_tensors
         R, S = z.shape
         if g_rgb is None:
@@ -286,6 +305,29 @@ class PackedMLP:
             raise ValueError("expected the 24 parameters of one NeRF in state_dict order")
         self.params = list(params)
         self._cache = {}
+        # called as grad_ready(flat_grad_view) once this net's gradient is complete in a
+        # backward pass (the data-parallel trainer starts its all-reduce bucket there)
+        self.grad_ready = None
+
+    def flat_grad(self) -> Optional[torch.Tensor]:
+        """The 24 .grad tensors as one flat fp32 view, when they are laid out back to back in
+        state_dict order (FusedAdam's flat buffer); else None."""
+        gs = [p.grad for p in self.params]
+        if any(g is None for g in gs):
+            return None
+        g0 = gs[0]
+        if g0.dtype != torch.float32 or not g0.is_cuda:
+            return None
+        base, st = g0.data_ptr(), g0.untyped_storage().data_ptr()
+        off = 0
+        for g in gs:
+            if (g.dtype != torch.float32 or not g.is_contiguous() or g.untyped_storage().data_ptr() != st
+                    or g.data_ptr() != base + 4 * off):
+                return None
+            off += g.numel()
+        start = (base - st) // 4
+        return torch.empty(0, dtype=torch.float32, device=g0.device).set_(
+            g0.untyped_storage(), start, (off,), (1,))
 
     def _key(self):
         return (_PARAM_GENERATION[0],) + tuple((p.data_ptr(), p._version) for p in self.params)
@@ -351,7 +393,11 @@ class _MLP(torch.autograd.Function):
         dev = g_raw.device
         g_raw = g_raw.contiguous()
         dz = torch.empty(lib().nerf_mlp_dz_bytes(ctx.dtype, ctx.M), dtype=torch.uint8, device=dev)
-        grad = torch.zeros(lib().nerf_mlp_net_params(), device=dev, dtype=torch.float32)
+        # accumulate straight into the parameters' .grad when they are one flat buffer (the
+        # dW kernel adds with atomics): no zero-fill, no 24 autograd accumulation kernels
+        direct = ctx.packer.flat_grad()
+        grad = direct if direct is not None else torch.zeros(lib().nerf_mlp_net_params(), device=dev,
+                                                              dtype=torch.float32)
         s = stream_of(g_raw)
         with kernel_timer("mlp_bwd_dx", ctx.M):
             check(lib().nerf_mlp_bwd_dx(ptr(ctx.packed_bwd), ctx.dtype, ptr(g_raw), ctx.M, ptr(ctx.masks), ptr(dz), s),
@@ -359,6 +405,10 @@ class _MLP(torch.autograd.Function):
         with kernel_timer("mlp_bwd_dw", ctx.M):
             check(lib().nerf_mlp_bwd_dw(ctx.dtype, ctx.M, ptr(ctx.act), ptr(dz), ptr(grad), s), "nerf_mlp_bwd_dw")
         ctx.act = ctx.masks = None
+        if ctx.packer.grad_ready is not None:
+            ctx.packer.grad_ready(grad if direct is not None else None)
+        if direct is not None:
+            return nones + (None,) * len(params)
         out, off = [], 0
         for p in params:
             n = p.numel()

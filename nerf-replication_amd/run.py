@@ -3,6 +3,10 @@
     python run.py --type evaluate --cfg_file configs/nerf/lego.yaml   # grid-accelerated render + PSNR/SSIM
     python run.py --type network  --cfg_file configs/nerf/lego.yaml   # hierarchical render timing
     python run.py --type dataset  --cfg_file configs/nerf/lego.yaml
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 run.py --type evaluate ...
+
+Under torch.distributed.run every image is split into contiguous ray blocks, one per GPU,
+and gathered after rendering (src/utils/dist_render.py); rank 0 evaluates and prints.
 """
 import os
 import sys
@@ -23,12 +27,25 @@ def run_dataset():
         pass
 
 
+def _init_dist():
+    """RCCL process group when launched by torch.distributed.run; returns the rank."""
+    import torch.distributed as dist
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not dist.is_initialized():
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
+    return dist.get_rank() if dist.is_initialized() else 0
+
+
 def run_network():
     from src.datasets import make_data_loader
     from src.models import make_network
     from src.models.nerf.renderer import make_renderer
     from src.utils.net_utils import load_network
 
+    from src.utils.dist_render import render_distributed
+
+    rank = _init_dist()
     network = make_network(cfg).cuda()
     load_network(network, cfg.trained_model_dir, epoch=cfg.test.epoch)
     network.eval()
@@ -39,10 +56,11 @@ def run_network():
         with torch.no_grad():
             torch.cuda.synchronize()
             t0 = time.time()
-            renderer.render(batch)
+            render_distributed(renderer, batch)
             torch.cuda.synchronize()
             total += time.time() - t0
-    print(total / len(loader))
+    if rank == 0:
+        print(total / len(loader))
 
 
 def run_evaluate():
@@ -52,7 +70,11 @@ def run_evaluate():
     from src.models.nerf.renderer import make_renderer
     from src.utils.net_utils import load_network
 
-    print(f"trained_model_dir: {cfg.trained_model_dir}")
+    from src.utils.dist_render import render_distributed
+
+    rank = _init_dist()
+    if rank == 0:
+        print(f"trained_model_dir: {cfg.trained_model_dir}")
     network = make_network(cfg).cuda()
     load_network(network, cfg.trained_model_dir, resume=cfg.resume, epoch=cfg.test.epoch)
     network.eval()
@@ -67,14 +89,16 @@ def run_evaluate():
         with torch.no_grad():
             torch.cuda.synchronize()
             t0 = time.time()
-            output = renderer.render_accelerated(batch)
+            output = render_distributed(renderer, batch, accelerated=True)
             torch.cuda.synchronize()
             net_time.append(time.time() - t0)
-        evaluator.evaluate(output, batch)
-    evaluator.summarize()
-    t = np.mean(net_time[1:]) if len(net_time) > 1 else np.mean(net_time)
-    print("net_time: ", t)
-    print("fps: ", 1.0 / t)
+        if rank == 0:
+            evaluator.evaluate(output, batch)
+    if rank == 0:
+        evaluator.summarize()
+        t = np.mean(net_time[1:]) if len(net_time) > 1 else np.mean(net_time)
+        print("net_time: ", t)
+        print("fps: ", 1.0 / t)
 
 
 if __name__ == "__main__":

@@ -108,8 +108,8 @@ class Dataset:
             rays, rgbs = self.image_rays(index)
             ret = {"rays": rays[None], "rgbs": rgbs[None], "H": torch.tensor([self.H]),
                    "W": torch.tensor([self.W]), "focal": torch.tensor([self.focal])}
-        ret["near"] = torch.tensor([float(cfg.task_arg.near)], device=self.device)
-        ret["far"] = torch.tensor([float(cfg.task_arg.far)], device=self.device)
+        ret["near"] = ops.device_scalar(float(cfg.task_arg.near), self.device)
+        ret["far"] = ops.device_scalar(float(cfg.task_arg.far), self.device)
         ret["i"] = torch.tensor([index])
         return ret
 

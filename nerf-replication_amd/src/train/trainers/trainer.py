@@ -1,11 +1,13 @@
 """Trainer (reference: src/train/trainers/trainer.py:11-130), data-parallel on RCCL.
 
 The reference wraps the loss module in DistributedDataParallel (trainer.py:15-22).  Here
-every rank draws its own rays (rank-distinct Philox streams), and after backward the
-whole gradient -- one flat fp32 buffer owned by FusedAdam (1,191,688 values, 4.77 MB) --
-is averaged with a single all-reduce (RCCL over xGMI on GPUs, gloo on CPU tests).  Initial
-weights are broadcast from rank 0, as DDP does at construction.  The clip_grad_value_(40)
-of trainer.py:61 is fused into the Adam launch.
+every rank draws its own rays (rank-distinct Philox streams), and the gradient -- one flat
+fp32 buffer owned by FusedAdam (1,191,688 values, 4.77 MB) -- is averaged across ranks in
+two buckets, one per NeRF: each net's MLP backward reports its finished flat gradient
+(PackedMLP.grad_ready) and that bucket's all-reduce starts at once on the collective
+stream, so the fine net's reduction (its backward runs first) overlaps the coarse net's
+backward.  Initial weights are broadcast from rank 0, as DDP does at construction.  The
+clip_grad_value_(40) of trainer.py:61 is fused into the Adam launch.
 """
 import datetime
 import time
@@ -35,6 +37,47 @@ def allreduce_grads(optimizer) -> None:
         g.mul_(1.0 / dist_world())
 
 
+class GradBuckets:
+    """Per-net all-reduce buckets started from inside backward.
+
+    ``attach(packers)`` installs a grad_ready hook on every NeRF's PackedMLP; a hook fires
+    when that net's dW has been enqueued into its slice of the flat gradient and starts an
+    async SUM all-reduce of the slice.  ``finish(optimizer)`` waits for the started buckets,
+    all-reduces whatever did not report (a net whose grads are not flat views, or that did
+    not run), and divides by the world size."""
+
+    def __init__(self):
+        self.works = []
+        self.done = []
+
+    def attach(self, packers):
+        for pk in packers:
+            pk.grad_ready = self._hook
+
+    def _hook(self, flat):
+        if flat is None or dist_world() == 1:
+            return
+        self.works.append(dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True))
+        self.done.append((flat.data_ptr(), flat.numel()))
+
+    def finish(self, optimizer) -> None:
+        world = dist_world()
+        if world == 1:
+            return
+        for w in self.works:
+            w.wait()
+        g = optimizer.flat_grad
+        base = g.data_ptr()
+        covered = sorted(((p - base) // 4, n) for p, n in self.done)
+        pos = 0
+        for off, n in covered + [(g.numel(), 0)]:
+            if off > pos:  # a range nobody reported: reduce it now
+                dist.all_reduce(g[pos:off], op=dist.ReduceOp.SUM)
+            pos = max(pos, off + n)
+        g.mul_(1.0 / world)
+        self.works, self.done = [], []
+
+
 class Trainer:
     def __init__(self, network):
         device = torch.device("cuda", cfg.local_rank) if torch.cuda.is_available() else torch.device("cpu")
@@ -44,6 +87,9 @@ class Trainer:
         self.device = device
         self.global_step = 0
         self.clip_value = 40.0
+        self.buckets = GradBuckets()
+        if dist_world() > 1:
+            self.buckets.attach([m.packer() for m in self.network.modules() if hasattr(m, "packer")])
 
     def reduce_loss_stats(self, loss_stats):
         return {k: torch.mean(v) for k, v in loss_stats.items()}
@@ -64,8 +110,8 @@ class Trainer:
         output, loss, loss_stats = self.network(batch)
         loss = loss.mean()
         optimizer.zero_grad()
-        loss.backward()
-        allreduce_grads(optimizer)
+        loss.backward()  # per-net all-reduce buckets start inside (GradBuckets)
+        self.buckets.finish(optimizer)
         optimizer.clip_value = self.clip_value
         optimizer.step()
         return output, loss, loss_stats

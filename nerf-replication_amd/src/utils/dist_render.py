@@ -1,0 +1,57 @@
+"""Multi-GPU inference: one image's rays split into contiguous row blocks, one per rank,
+rendered independently, then gathered (640,000 rays / 8 = 80,000 per GPU;
+rgb/depth/acc gathered at the end, no other collective).
+
+Used by run.py --type evaluate|network under torch.distributed.run; the renderer is any
+object with render / render_accelerated (the reference's Renderer interface)."""
+import torch
+import torch.distributed as dist
+
+
+def _world():
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def shard_bounds(n: int, rank: int, world: int):
+    """[start, stop) of rank's contiguous share of n rays (sizes differ by at most one)."""
+    return n * rank // world, n * (rank + 1) // world
+
+
+def render_distributed(renderer, batch, accelerated: bool = False, keys=None):
+    """Render batch['rays'] split across ranks; every rank returns the full outputs.
+
+    Each rank renders rays [n r / W, n (r + 1) / W); per-ray outputs ([N] or [N, c]
+    tensors) are padded to the largest share and all_gathered, then trimmed; scalars
+    (render_time, n_queried) are max- / sum-reduced."""
+    world = _world()
+    fn = renderer.render_accelerated if accelerated else renderer.render
+    if world == 1:
+        return fn(batch)
+    rank = dist.get_rank()
+    rays = batch["rays"]
+    flat = rays.reshape(-1, 6)
+    n = flat.shape[0]
+    a, b = shard_bounds(n, rank, world)
+    sub = dict(batch)
+    sub["rays"] = flat[a:b][None] if rays.dim() == 3 else flat[a:b]
+    out = fn(sub)
+    share = (n + world - 1) // world
+    res = {}
+    for k, v in out.items():
+        if keys is not None and k not in keys:
+            continue
+        if torch.is_tensor(v) and v.dim() >= 1 and v.shape[0] == b - a:
+            pad = torch.zeros((share,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+            pad[: b - a] = v
+            parts = [torch.empty_like(pad) for _ in range(world)]
+            dist.all_gather(parts, pad)
+            res[k] = torch.cat([parts[r][: shard_bounds(n, r, world)[1] - shard_bounds(n, r, world)[0]]
+                                for r in range(world)], 0)
+        elif isinstance(v, (int, float)):
+            dev = flat.device if flat.device.type != "cpu" or dist.get_backend() == "gloo" else "cuda"
+            t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM if k == "n_queried" else dist.ReduceOp.MAX)
+            res[k] = type(v)(t.item())
+        else:
+            res[k] = v
+    return res

@@ -1,8 +1,10 @@
 """CPU, world_size 2 (gloo): the data-parallel step's collective semantics.
 
-Each rank holds a flat gradient (FusedAdam.flat_grad's role); allreduce_grads must leave
-every rank with the mean, and broadcast_params must give every rank rank-0's weights
-(DistributedDataParallel's construction broadcast, trainer.py:15-22 of the reference).
+Each rank holds a flat gradient (FusedAdam.flat_grad's role); allreduce_grads and the
+per-net GradBuckets (started from backward, remainder in finish) must leave every rank
+with the mean; broadcast_params must give every rank rank-0's weights
+(DistributedDataParallel's construction broadcast, trainer.py:15-22 of the reference); the
+tile-split renderer must reproduce a single-process render.
 """
 import os
 import socket
@@ -21,6 +23,17 @@ def _free_port():
     return p
 
 
+class _FakeRenderer:
+    """rgb / depth / acc as fixed functions of each ray (the split/gather logic under test)."""
+
+    def render(self, batch):
+        r = batch["rays"].reshape(-1, 6)
+        return {"rgb_map_f": r[:, :3] * 2.0, "depth_map_f": r[:, 3] + 1.0, "acc_map_f": r[:, 4],
+                "n_queried": int(r.shape[0])}
+
+    render_accelerated = render
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       NERF_AMD_NO_ARGV="1")
@@ -36,10 +49,24 @@ def _worker(rank, world, port, q):
     opt = Opt()
     opt.flat_grad = torch.arange(10, dtype=torch.float32) * (rank + 1)
     allreduce_grads(opt)
+    opt_grad_plain = opt.flat_grad.tolist()
     lin = torch.nn.Linear(4, 3)
     torch.nn.init.constant_(lin.weight, float(rank))
     broadcast_params(lin)
-    q.put((rank, opt.flat_grad.tolist(), float(lin.weight.sum())))
+    # per-net buckets: one slice reported from "backward", the rest reduced in finish()
+    from src.train.trainers.trainer import GradBuckets
+    opt.flat_grad = torch.arange(10, dtype=torch.float32) * (rank + 1)
+    bk = GradBuckets()
+    bk._hook(opt.flat_grad[2:6])
+    bk.finish(opt)
+    bucket_grad = opt.flat_grad.tolist()
+    # tile-split inference: 1001 rays over the ranks, gathered everywhere
+    from src.utils.dist_render import render_distributed
+    rays = torch.arange(1001 * 6, dtype=torch.float32).reshape(1, 1001, 6)
+    full = _FakeRenderer().render({"rays": rays})
+    got = render_distributed(_FakeRenderer(), {"rays": rays})
+    ok = all(torch.equal(got[k], full[k]) for k in ("rgb_map_f", "depth_map_f", "acc_map_f"))
+    q.put((rank, opt_grad_plain, float(lin.weight.sum()), bucket_grad, ok and got["n_queried"] == 1001))
     dist.destroy_process_group()
 
 
@@ -55,6 +82,8 @@ def test_two_rank_gradient_average_and_broadcast():
         p.join(timeout=60)
         assert p.exitcode == 0
     expect = [1.5 * i for i in range(10)]
-    for rank, grad, wsum in res:
+    for rank, grad, wsum, bucket_grad, render_ok in res:
         assert grad == pytest.approx(expect)
         assert wsum == 0.0  # rank 0's weights everywhere
+        assert bucket_grad == pytest.approx(expect)  # bucketed + remainder == one flat average
+        assert render_ok  # tile-split render == single-process render
