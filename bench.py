@@ -32,6 +32,12 @@ METRIC = "train rays/sec (fwd+bwd, 64+128 samples) + 800x800 render s/frame, 1/2
 # (no input grad for PE(xyz) at layers 0/5 and PE(dir) at the view layer), dW 593,408 MAC
 FLOP_PER_SAMPLE = {"mlp_fwd_train": 2 * 593408, "mlp_fwd": 2 * 593408, "mlp_bwd_dx": 2 * 557696,
                    "mlp_bwd_dw": 2 * 593408}
+# the dW GEMMs stream the training stores once: every stored activation tile (79 x 32 rows)
+# and output-gradient tile (78 x 32 rows) of a sample, 2 B (bf16) / 4 B (fp32) per value
+# (DESIGN.md 4); that makes dW HBM-bound, the other MLP kernels MFMA-bound
+STORE_ROWS = (79 + 78) * 32
+BOUND = {"mlp_fwd_train": "mfma", "mlp_fwd": "mfma", "mlp_bwd_dx": "mfma", "mlp_bwd_dw": "hbm"}
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
 
 
@@ -185,14 +191,30 @@ def main():
 
     rays_total = world * args.rays * args.steps
     value = rays_total / elapsed
-    # dominant kernel: largest total device time among the MLP kernels
+    # dominant kernel: largest total device time among the MLP kernels, priced against the
+    # roofline that bounds it
+    esize = 2 if args.dtype == "bf16" else 4
+
+    def roof(k, n, ms, units):
+        avg_ms = ms / n
+        if BOUND[k] == "hbm":
+            per = STORE_ROWS * esize * units / n
+            ach = per / (avg_ms * 1e-3) / 1e9
+            return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(ach / PEAK_HBM_GBS, 4), "bytes_per_launch": per, "avg_launch_ms": round(avg_ms, 4)}
+        per = FLOP_PER_SAMPLE[k] * units / n
+        ach = per / (avg_ms * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s",
+                "frac": round(ach / PEAK_TFLOPS[args.dtype], 4), "flop_per_launch": per,
+                "avg_launch_ms": round(avg_ms, 4)}
+
     name, (n_launch, ms, units) = max(ktimes.items(), key=lambda kv: kv[1][1])
-    avg_ms = ms / n_launch
-    flop_per_launch = FLOP_PER_SAMPLE.get(name, 0) * units / n_launch
-    achieved = flop_per_launch / (avg_ms * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic(name, args.dtype)
+    roofline = dict(kernel=name, **roof(name, n_launch, ms, units), traffic=traffic,
+                    traffic_unit="HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)", traffic_source=traffic_src)
     kt = {k: {"launches": n, "avg_ms": round(m / n, 4), "samples_per_launch": u // n,
-              "tflops": round(FLOP_PER_SAMPLE.get(k, 0) * (u / n) / (m / n * 1e-3) / 1e12, 2)}
+              "tflops": round(FLOP_PER_SAMPLE.get(k, 0) * (u / n) / (m / n * 1e-3) / 1e12, 2),
+              "roofline": roof(k, n, m, u)}
           for k, (n, m, u) in ktimes.items()}
 
     render_s = None
@@ -212,11 +234,7 @@ def main():
                                    "MSE(c)+MSE(f), clip 40 + Adam",
                        "rays_per_gpu": args.rays, "global_batch_rays": args.rays * world,
                        "samples_per_ray": 64 + 192, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2),
-                         "peak": PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_TFLOPS[args.dtype], 4), "traffic": traffic,
-                         "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
-                         "flop_per_launch": flop_per_launch, "avg_launch_ms": round(avg_ms, 4)},
+            "roofline": roofline,
             "kernels": kt,
             "render_s_per_frame": None if render_s is None else round(render_s, 4),
             "cpu_baseline": cpu,
