@@ -111,9 +111,9 @@ def positional_encoding(x: torch.Tensor, n_freqs: int) -> torch.Tensor:
 
     Frequencies are 2.**linspace(0, L-1, L) (exact powers of two).
     """
-    bands = 2.0 ** torch.linspace(0.0, n_freqs - 1, steps=n_freqs)
+    bands = 2.0 ** torch.linspace(0.0, n_freqs - 1, steps=n_freqs)  # CPU table (exact powers of two)
     parts = [x]
-    for f in bands:
+    for f in bands.to(x.device):
         parts.append(torch.sin(x * f))
         parts.append(torch.cos(x * f))
     return torch.cat(parts, -1)
@@ -161,12 +161,12 @@ def composite(raw: torch.Tensor, z: torch.Tensor, rays_d: torch.Tensor, white_bk
     Returns rgb [R,3], depth [R], acc [R], weights [R,S].
     """
     delta = z[..., 1:] - z[..., :-1]
-    delta = torch.cat([delta, torch.tensor([1e10]).expand(delta[..., :1].shape)], -1)
+    delta = torch.cat([delta, torch.tensor([1e10], device=z.device).expand(delta[..., :1].shape)], -1)
     delta = delta * torch.norm(rays_d[..., None, :], dim=-1)
     color = torch.sigmoid(raw[..., :3])
     sigma = F.relu(raw[..., 3])
     alpha = 1.0 - torch.exp(-sigma * delta)
-    ones = torch.ones((alpha.shape[0], 1))
+    ones = torch.ones((alpha.shape[0], 1), device=alpha.device)
     trans = torch.cumprod(torch.cat([ones, 1.0 - alpha + 1e-10], -1), -1)[:, :-1]
     w = alpha * trans
     rgb = torch.sum(w[..., None] * color, -2)
@@ -193,9 +193,9 @@ def sample_pdf(bins: torch.Tensor, weights: torch.Tensor, n: int, det: bool,
     cdf = torch.cat([torch.zeros_like(pdf[..., :1]), torch.cumsum(pdf, -1)], -1)
     if u is None:
         if det:
-            u = torch.linspace(0.0, 1.0, steps=n).expand(list(cdf.shape[:-1]) + [n])
+            u = torch.linspace(0.0, 1.0, steps=n).to(cdf.device).expand(list(cdf.shape[:-1]) + [n])
         else:
-            u = torch.rand(list(cdf.shape[:-1]) + [n])
+            u = torch.rand(list(cdf.shape[:-1]) + [n], device=cdf.device)
     u = u.contiguous()
     inds = torch.searchsorted(cdf, u, right=True)
     lo = torch.clamp(inds - 1, min=0)
@@ -229,9 +229,11 @@ def samples_from_cdf(bins: torch.Tensor, cdf: torch.Tensor, u: torch.Tensor):
     return bb + t * (ba - bb), inds
 
 
-def stratified_z(n_rays: int, near, far, n: int = N_SAMPLES, t_rand: Optional[torch.Tensor] = None):
+def stratified_z(n_rays: int, near, far, n: int = N_SAMPLES, t_rand: Optional[torch.Tensor] = None, device=None):
     """Stratified depths (volume_renderer.py:165-181); t_rand given => perturbed."""
-    t = torch.linspace(0.0, 1.0, steps=n, dtype=torch.float32)
+    t = torch.linspace(0.0, 1.0, steps=n, dtype=torch.float32).to(device or "cpu")  # CPU linspace, as the reference
+    if torch.is_tensor(near):
+        near, far = near.to(t.device), far.to(t.device)
     z = near * (1.0 - t) + far * t
     z = z.expand([n_rays, n])
     if t_rand is not None:
@@ -260,8 +262,8 @@ def render(coarse, fine, rays: torch.Tensor, near, far, perturb: bool = False,
         R = o.shape[0]
         tr = None
         if perturb:
-            tr = t_rand[s:s + chunk] if t_rand is not None else torch.rand([R, N_SAMPLES])
-        z = stratified_z(R, near, far, N_SAMPLES, tr)
+            tr = t_rand[s:s + chunk] if t_rand is not None else torch.rand([R, N_SAMPLES], device=rc.device)
+        z = stratified_z(R, near, far, N_SAMPLES, tr, device=rc.device)
         pts = o[..., None, :] + d[..., None, :] * z[..., :, None]
         vd = d / torch.norm(d, dim=-1, keepdim=True)
         raw_c = network_forward(coarse, pts, vd)
