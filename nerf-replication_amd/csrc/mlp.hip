@@ -95,6 +95,33 @@ struct PBF16 {
   static __device__ __forceinline__ uint4 chunk(const Tile& t, int c) { return __builtin_bit_cast(uint4, t.b[c]); }
 };
 
+// ReLU-mask bit of accumulator register rho of a tile: the tile's 16 bits sit at positions
+// (rho >> 1) + 16 (rho & 1) of a dword (bf16 pair k = registers 2k, 2k+1 -> bits k, 16 + k),
+// and two tiles n, n + 1 share one dword, the odd one shifted up by 8.
+__host__ __device__ constexpr int mask_bit(int rho) { return (rho >> 1) + 16 * (rho & 1); }
+#ifndef NERF_MASK_FROM_PACKED
+#define NERF_MASK_FROM_PACKED 0
+#endif
+
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(2))) short i16x2;
+typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
+
+// registers 2k, 2k+1 of an fp32 accumulator as one packed bf16 pair (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
+}
+// ReLU of a bf16 pair: sign-magnitude bf16 ordered as int16 -> v_pk_max_i16 with 0
+// (relu(bf16(x)) == bf16(relu(x)): rounding keeps the sign)
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t d) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2, d), (i16x2){0, 0}));
+}
+// 1 in each half that is non-zero (v_pk_min_u16 with 1)
+__device__ __forceinline__ uint32_t nonzero_bf16x2(uint32_t d) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, d), (u16x2){1, 1}));
+}
+
 template <class P> __host__ __device__ constexpr int samples_per_block() { return P::WAVES * 32; }
 constexpr int M_ALIGN = 256;  // activation stores are padded to this many samples
 
@@ -503,8 +530,8 @@ __device__ __forceinline__ void store_tile(void* base, int64_t nblk, int ntiles,
 
 // ReLU masks of the training forward, read by the dX chain: per 32-sample wave block,
 // MASK_GROUPS x 64 lanes x 16 B; group l < 8 = layer l's 8 output tiles (tile n -> dword
-// n >> 1, bits 16 (n & 1) + rho), group 8 = the view layer's 4 tiles.  One 16-byte store
-// per lane per layer.
+// n >> 1, bit 8 (n & 1) + mask_bit(rho)), group 8 = the view layer's 4 tiles.  One 16-byte
+// store per lane per layer.
 __device__ __forceinline__ uint4* mask_slot(void* masks, int64_t wblock, int grp, int lane) {
   return (uint4*)masks + (wblock * MASK_GROUPS + grp) * 64 + lane;
 }
@@ -593,20 +620,39 @@ struct FwdWave {
   template <int L, int n> __device__ __forceinline__ void finish_L(const f32x16& acc) {
     if constexpr (L <= L7 || L == LV) {
       Tile out;
-      uint32_t bits = 0;
+      uint32_t bits = 0;  // mask bits of this tile (mask_bit layout)
+      if constexpr (P::CH == 2) {
+        // bf16: pack pairs first, then ReLU and mask on the packed pairs (2 values per VALU)
+        uint32_t d[8];
 #pragma unroll
-      for (int rho = 0; rho < 16; ++rho) {
-        // ReLU as an integer max on the float bits (negative floats are negative ints): one
-        // v_max_i32, no NaN canonicalisation; mask bit = (x > 0) = min(relu bits, 1)
-        const int y = max(__float_as_int(acc[rho]), 0);
-        if constexpr (STORE) bits |= min((uint32_t)y, 1u) << rho;
-        P::set(out, rho, __int_as_float(y));
+        for (int k = 0; k < 8; ++k) {
+#if NERF_MASK_FROM_PACKED
+          d[k] = relu_bf16x2(pack_bf16(acc[2 * k], acc[2 * k + 1]));
+          if constexpr (STORE) bits |= nonzero_bf16x2(d[k]) << k;
+#else
+          if constexpr (STORE) {
+            bits |= (acc[2 * k] > 0.f ? 1u : 0u) << mask_bit(2 * k);
+            bits |= (acc[2 * k + 1] > 0.f ? 1u : 0u) << mask_bit(2 * k + 1);
+          }
+          d[k] = relu_bf16x2(pack_bf16(acc[2 * k], acc[2 * k + 1]));
+#endif
+        }
+        out.b[0] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
+        out.b[1] = __builtin_bit_cast(bf16x8, make_uint4(d[4], d[5], d[6], d[7]));
+      } else {
+#pragma unroll
+        for (int rho = 0; rho < 16; ++rho) {
+          // ReLU as an integer max on the float bits (negative floats are negative ints)
+          const int y = max(__float_as_int(acc[rho]), 0);
+          if constexpr (STORE) bits |= (y > 0 ? 1u : 0u) << mask_bit(rho);
+          P::set(out, rho, __int_as_float(y));
+        }
       }
       out_arr<L>()[n] = out;
       if constexpr (STORE) {
         store_tile<P>(a.act, a.nblk, AT_TILES, (L == LV ? AT_V : AT_H + 8 * L) + n, wblock, lane, out);
         if constexpr ((n & 1) == 0) mw[n >> 1] = bits;
-        else mw[n >> 1] |= bits << 16;
+        else mw[n >> 1] |= bits << 8;
         if constexpr (n == fwd_out_tiles(L) - 1)
           *mask_slot(a.masks, wblock, L == LV ? 8 : L, lane) =
               make_uint4(mw[0], mw[1], L == LV ? 0u : mw[2], L == LV ? 0u : mw[3]);
@@ -614,8 +660,16 @@ struct FwdWave {
     } else if constexpr (L == LFA) {
       if constexpr (n < 8) {  // feature_linear: no activation
         Tile out;
+        if constexpr (P::CH == 2) {
+          uint32_t d[8];
 #pragma unroll
-        for (int rho = 0; rho < 16; ++rho) P::set(out, rho, acc[rho]);
+          for (int k = 0; k < 8; ++k) d[k] = pack_bf16(acc[2 * k], acc[2 * k + 1]);
+          out.b[0] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
+          out.b[1] = __builtin_bit_cast(bf16x8, make_uint4(d[4], d[5], d[6], d[7]));
+        } else {
+#pragma unroll
+          for (int rho = 0; rho < 16; ++rho) P::set(out, rho, acc[rho]);
+        }
         Ha[n] = out;
         if constexpr (STORE) store_tile<P>(a.act, a.nblk, AT_TILES, AT_F + n, wblock, lane, out);
       } else {
@@ -802,14 +856,26 @@ struct DxWave {
   template <int u> __device__ __forceinline__ void finish(const f32x16& acc) {
     constexpr int s = bwd_unit_stage(u), j = u - bwd_unit_first(s);
     constexpr int mg = mask_group(s);
-    uint32_t mask = 0xFFFFu;
+    uint32_t w = 0xFFFFFFFFu;  // this tile's bits at mask_bit(rho)
     if constexpr (mg >= 0) {
-      const uint32_t w = (j >> 1) == 0 ? mk[mg].x : (j >> 1) == 1 ? mk[mg].y : (j >> 1) == 2 ? mk[mg].z : mk[mg].w;
-      mask = (j & 1) ? (w >> 16) : (w & 0xFFFFu);
+      w = (j >> 1) == 0 ? mk[mg].x : (j >> 1) == 1 ? mk[mg].y : (j >> 1) == 2 ? mk[mg].z : mk[mg].w;
+      w >>= 8 * (j & 1);
     }
     Tile out;
+    if constexpr (P::CH == 2) {
+      uint32_t d[8];
 #pragma unroll
-    for (int rho = 0; rho < 16; ++rho) P::set(out, rho, ((mask >> rho) & 1u) ? acc[rho] : 0.f);
+      for (int k = 0; k < 8; ++k) {
+        d[k] = pack_bf16(acc[2 * k], acc[2 * k + 1]);
+        // bits k, 16 + k -> 0x0000FFFF / 0xFFFF0000 halves (one v_mul_u32_u24)
+        if constexpr (mg >= 0) d[k] &= ((w >> k) & 0x10001u) * 0xFFFFu;
+      }
+      out.b[0] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
+      out.b[1] = __builtin_bit_cast(bf16x8, make_uint4(d[4], d[5], d[6], d[7]));
+    } else {
+#pragma unroll
+      for (int rho = 0; rho < 16; ++rho) P::set(out, rho, ((w >> mask_bit(rho)) & 1u) ? acc[rho] : 0.f);
+    }
     out_arr<s>()[j] = out;
     constexpr int dzt = dz_tile(s, j);
     store_tile<P>(a.dz, a.nblk, ZT_TILES, dzt, wblock, lane, out);

@@ -221,21 +221,21 @@ def test_mlp_backward(cuda, ops, O, seeded_state, dtype):
 
 
 def _decode_masks(masks_u8, M):
-    """ReLU masks [nblk, 9 groups, 64 lanes, 4 dwords] (group l < 8: layer l, tile n in dword
-    n >> 1 at bit 16 (n & 1) + rho; group 8: the view layer's 4 tiles; bit rho of lane l =
-    sample 32 blk + (l & 31), feature acc_row(rho, l >> 5) of the tile) -> {tile: bool [M, 32]}
-    with tile 8 l + n for the trunk and 64 + n for the view layer."""
+    """ReLU masks [nblk, 9 groups, 64 lanes, 4 dwords] (group l < 8: layer l, group 8: the view
+    layer; tile n in dword n >> 1, register rho at bit 8 (n & 1) + (rho >> 1) + 16 (rho & 1);
+    lane l = sample 32 blk + (l & 31), register rho = feature acc_row(rho, l >> 5) of the tile)
+    -> {tile: bool [M, 32]} with tile 8 l + n for the trunk and 64 + n for the view layer."""
     w = masks_u8.view(torch.int32).cpu().numpy().view(np.uint32).reshape(-1, 9, 64, 4)
-    tiles = []
+    nblk = w.shape[0]
+    out = np.zeros((nblk, 68, 32, 32), dtype=bool)  # [blk, tile, sample, feature]
     for t in range(68):
         grp, n = (t // 8, t % 8) if t < 64 else (8, t - 64)
-        tiles.append(((w[:, grp, :, n >> 1] >> (16 * (n & 1))) & 0xFFFF).astype(np.uint16))
-    m = np.stack(tiles, 1)  # [nblk, 68, 64]
-    bits = (m[..., None] >> np.arange(16, dtype=np.uint16)) & 1  # [nblk, 68, 64, 16]
-    out = np.zeros((m.shape[0], 68, 32, 32), dtype=bool)  # [blk, tile, sample, feature]
-    for lane in range(64):
+        word = w[:, grp, :, n >> 1]  # [nblk, 64]
         for rho in range(16):
-            out[:, :, lane & 31, (rho & 3) + 8 * (rho >> 2) + 4 * (lane >> 5)] = bits[:, :, lane, rho]
+            bit = 8 * (n & 1) + (rho >> 1) + 16 * (rho & 1)
+            b = ((word >> bit) & 1).astype(bool)
+            for h in range(2):
+                out[:, t, :, (rho & 3) + 8 * (rho >> 2) + 4 * h] = b[:, 32 * h:32 * h + 32]
     out = out.transpose(1, 0, 2, 3).reshape(68, -1, 32)[:, :M]
     return torch.from_numpy(out)
 

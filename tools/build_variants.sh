@@ -10,7 +10,7 @@ pids=()
 while [ $# -gt 1 ]; do
   name=$1; defs=$2; shift 2
   (
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$ROOT/include $defs -c $CS/mlp.hip -o /tmp/var_$name.o &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$ROOT/include $defs -c ${SRC:-$CS/mlp.hip} -o /tmp/var_$name.o &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/variants/$name.so /tmp/var_$name.o \
       $ROOT/build/nerf_amd/sampling.hip.o $ROOT/build/nerf_amd/grid.hip.o $ROOT/build/nerf_amd/optim.hip.o $ROOT/build/nerf_amd/errors.cpp.o
   ) &
