@@ -132,6 +132,49 @@ def render_frame_time(cfg, net, ds, device, reps=2):
     return min(times)
 
 
+def grid_times(cfg, net, ds, device, reps=2):
+    """BASELINE config 4: the 128^3 x 8-corner occupancy bake (occupancy_grid.py:15-80) and the
+    grid-accelerated 800x800 march (render_accelerated, volume_renderer.py:268-357) of test
+    view 0 through the reference's own baked lego grid (tests/golden/lego_occupancy_grid.npz,
+    packed bits of logs/lego/occupancy_grid.pt).  Weights are the synthetic seed-0 init."""
+    import numpy as np
+    from nerf_amd import ops
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    out = {}
+    with torch.no_grad():
+        def bake():
+            return ops.bake(net.model.packer(), 128, 1.0, dtype=cfg.task_arg.mlp_dtype)
+        bake()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            grid = bake()
+        torch.cuda.synchronize()
+        out["bake_s"] = round((time.perf_counter() - t0) / reps, 4)
+        out["bake_occupied"] = int(grid.sum())
+        z = np.load(os.path.join(ROOT, "tests", "golden", "lego_occupancy_grid.npz"), allow_pickle=False)
+        shape = tuple(int(v) for v in z["shape"])
+        lego = torch.from_numpy(np.unpackbits(z["packed"])[: int(np.prod(shape))].reshape(shape).astype(bool))
+        r = Renderer(net)
+        r.set_occupancy_grid(lego, device)
+        rays, _ = ds.image_rays(0)
+        batch = {"rays": rays, "near": ops.device_scalar(2.0, device), "far": ops.device_scalar(6.0, device)}
+        import contextlib
+        import io
+        with contextlib.redirect_stdout(io.StringIO()):
+            r.render_accelerated(batch)
+            times = []
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                o = r.render_accelerated(batch)
+                torch.cuda.synchronize()
+                times.append(time.perf_counter() - t0)
+        out["march_s_per_frame"] = round(min(times), 4)
+        out["march_queried_points"] = int(o["n_queried"])
+    return out
+
+
 def cpu_baseline(n_rays):
     """The oracle (tests-only CPU restatement of the reference, torch CPU) on a bounded
     sample: one n_rays forward+backward render (perturb 0), config 1 of BASELINE.json."""
@@ -217,9 +260,10 @@ def main():
               "roofline": roof(k, n, m, u)}
           for k, (n, m, u) in ktimes.items()}
 
-    render_s = None
+    render_s, grid = None, None
     if rank == 0 and not args.no_render and world == 1:
         render_s = render_frame_time(cfg, net, ds, device)
+        grid = grid_times(cfg, net, ds, device)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_rays)
@@ -237,6 +281,7 @@ def main():
             "roofline": roofline,
             "kernels": kt,
             "render_s_per_frame": None if render_s is None else round(render_s, 4),
+            "occupancy_grid": grid,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
