@@ -113,6 +113,15 @@ int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64
                     hipStream_t stream);
 int nerf_mlp_bwd_dw(int dtype, int64_t M, const void* act, const void* dz, float* grad, hipStream_t stream);
 
+/* ---- (a14) evaluator metrics (src/evaluators/nerf.py:23-45) --------------------------------------
+ * pred / gt fp32 [H,W,3] on the device -> out (device, 4 doubles): PSNR of the float images,
+ * SSIM of uint8(pred*255) vs uint8(gt*255) (7x7 uniform window, K1 0.01, K2 0.03, sample
+ * covariance, data_range = max - min of the uint8 prediction, 3-pixel crop, mean over channels),
+ * the sum of squared errors and the data range.  workspace: nerf_metrics_workspace_bytes(H, W). */
+int64_t nerf_metrics_workspace_bytes(int H, int W);
+int nerf_image_metrics(const float* pred, const float* gt, int H, int W, void* workspace, double* out,
+                       hipStream_t stream);
+
 /* ---- (a11) occupancy lookup ------------------------------------------------------------------
  * Replaces Renderer.world_to_grid_indices (volume_renderer.py:261-265) + the grid gather of
  * render_accelerated (:307-312).  bbox_host = {min xyz, max xyz} on the host. */

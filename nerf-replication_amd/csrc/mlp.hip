@@ -388,7 +388,6 @@ __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
   constexpr int PDP = prefetch_depth<P>();
   constexpr auto& T = GroupTable<DIR, DENSITY, P::CH>::t;
   constexpr Group G = T.g[g];
-  constexpr bool LASTG = g + 1 == T.n;
   constexpr int PREV_U = g > 0 ? T.g[g - 1].u0 + T.g[g - 1].n - 1 : -1;  // previous group's last unit
   uint4 ring[PDP];
   sfor<(NS < PDP ? NS : PDP)>([&](auto kk) {

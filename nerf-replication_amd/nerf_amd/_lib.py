@@ -54,6 +54,8 @@ SIGNATURES = {
                                  _p, _p, _p, _p, _p, _p, _i64, _p]),
     "nerf_march_composite": (_i32, [_p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _f32, _f32, _p]),
     "nerf_march_finish": (_i32, [_p, _p, _i64, _i32, _p]),
+    "nerf_metrics_workspace_bytes": (_i64, [_i32, _i32]),
+    "nerf_image_metrics": (_i32, [_p, _p, _i32, _i32, _p, _p, _p]),
     "nerf_adam_step": (_i32, [_p, _p, _p, _p, _i64, _f64, _f64, _f64, _f64, _i64, _f64, _p]),
 }
 

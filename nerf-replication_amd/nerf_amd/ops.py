@@ -546,6 +546,23 @@ def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: 
 
 
 # --------------------------------------------------------------------------------------
+# evaluator metrics
+# --------------------------------------------------------------------------------------
+def image_metrics(pred: torch.Tensor, gt: torch.Tensor):
+    """(psnr, ssim) of fp32 [H,W,3] device images (src/evaluators/nerf.py:23-45): PSNR on the
+    floats, skimage-default SSIM on uint8(x*255) with the prediction's uint8 range."""
+    pred, gt = _f32c(pred, "pred"), _f32c(gt, "gt")
+    if pred.dim() != 3 or pred.shape[-1] != 3 or pred.shape != gt.shape:
+        raise ValueError(f"image_metrics: expected two [H,W,3] images, got {tuple(pred.shape)} / {tuple(gt.shape)}")
+    H, W = int(pred.shape[0]), int(pred.shape[1])
+    ws = torch.empty(lib().nerf_metrics_workspace_bytes(H, W), dtype=torch.uint8, device=pred.device)
+    out = torch.empty(4, dtype=torch.float64, device=pred.device)
+    check(lib().nerf_image_metrics(ptr(pred), ptr(gt), H, W, ptr(ws), ptr(out), stream_of(pred)), "nerf_image_metrics")
+    o = out.tolist()
+    return o[0], o[1]
+
+
+# --------------------------------------------------------------------------------------
 # optimizer
 # --------------------------------------------------------------------------------------
 def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, lr: float,

@@ -7,6 +7,11 @@ this image, so ``structural_similarity`` is restated from its documented default
 K2 = 0.03, sample covariance N/(N-1), border of 3 px cropped before the mean, mean over
 channels).  Parity of this restatement with scikit-image is unpinned here (no skimage
 to compare against).  PNG dumps use PIL instead of cv2.
+
+When the rendered image is on the GPU the metrics run there (``nerf_image_metrics``,
+csrc/metrics.hip: exact integer window sums, fp64 SSIM formula); the numpy functions
+below are the same definitions on the host (used for host images and as the GPU
+kernel's test reference).
 """
 import json
 import os
@@ -59,10 +64,18 @@ class Evaluator:
         return ssim_metric_uint8((img_pred * 255).astype(np.uint8), img_gt)
 
     def evaluate(self, output, batch):
-        pred = output["rgb_map_f"].detach().float().cpu().numpy()
-        gt = batch["rgbs"].detach().float().cpu().numpy().reshape(-1, 3)
         i = int(batch["i"].reshape(-1)[0])
         H, W = int(batch["H"].reshape(-1)[0]), int(batch["W"].reshape(-1)[0])
+        pred_t = output["rgb_map_f"].detach().float()
+        gt_t = batch["rgbs"].detach().float()
+        if pred_t.is_cuda and gt_t.is_cuda and not self.save_images:
+            from nerf_amd import ops
+            psnr, ssim = ops.image_metrics(pred_t.reshape(H, W, 3), gt_t.reshape(H, W, 3))
+            self.psnr.append(psnr)
+            self.ssim.append(ssim)
+            return {"psnr": psnr, "ssim": ssim}
+        pred = pred_t.cpu().numpy()
+        gt = gt_t.cpu().numpy().reshape(-1, 3)
         img_pred, img_gt = pred.reshape(H, W, 3), gt.reshape(H, W, 3)
         psnr = self.psnr_metric(img_pred, img_gt)
         ssim = self.ssim_metric(img_pred, (img_gt * 255).astype(np.uint8), batch, i, 100)

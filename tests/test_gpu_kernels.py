@@ -326,3 +326,23 @@ def test_adam_matches_torch(cuda, ops):
         gg = gr.to(cuda)
         ops.adam_step(p, gg, m, v, 5e-4, step, clip_value=40.0)
     np.testing.assert_allclose(p.cpu().numpy(), p_ref.detach().numpy(), rtol=0, atol=1e-6)
+
+
+# ---------------------------------------------------------------------------------- evaluator
+@pytest.mark.parametrize("H,W,noise", [(800, 800, 0.05), (37, 53, 0.3), (64, 64, 0.0)])
+def test_image_metrics_match_host_evaluator(cuda, ops, H, W, noise):
+    """GPU PSNR/SSIM (csrc/metrics.hip) against the evaluator's numpy definitions
+    (src/evaluators/nerf.py, the reference's nerf.py:23-45 restated): SSIM to 1e-9, PSNR to
+    1e-4 dB (float32 vs float64 mean of the squared errors)."""
+    from src.evaluators.nerf import psnr_metric, ssim_metric_uint8
+    g = torch.Generator().manual_seed(H * W)
+    gt = torch.rand(H, W, 3, generator=g)
+    pred = (gt + noise * torch.randn(H, W, 3, generator=g)).clamp(0.0, 1.0)
+    if noise == 0.0:
+        pred[5:9, 7:11] = 0.5  # not identical: finite PSNR
+    psnr, ssim = ops.image_metrics(pred.to(cuda), gt.to(cuda))
+    p_np, g_np = pred.numpy(), gt.numpy()
+    ref_psnr = psnr_metric(p_np, g_np)
+    ref_ssim = ssim_metric_uint8((p_np * 255).astype(np.uint8), (g_np * 255).astype(np.uint8))
+    assert abs(psnr - ref_psnr) < 1e-4, (psnr, ref_psnr)
+    assert abs(ssim - ref_ssim) < 1e-9, (ssim, ref_ssim)
