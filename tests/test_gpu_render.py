@@ -170,3 +170,20 @@ def test_bake_lattice_exact_for_lego():
     from nerf_amd import ops
     assert ops.bake_lattice_exact(128)
     assert ops.bake_lattice_exact(8)
+
+
+def test_render_video_frames(cuda, stack):
+    """render_video.py (reference render_video.py:21-70): turntable poses, GPU ray
+    generation, hierarchical render; here 3 frames of a 48x48 camera, no files written."""
+    import render_video
+    cfg, _, _ = stack
+    H, W = cfg.test_dataset.H, cfg.test_dataset.W
+    cfg.test_dataset.H, cfg.test_dataset.W = 48, 48
+    try:
+        frames = render_video.render_360_video(num_frames=3, write=False)
+    finally:
+        cfg.test_dataset.H, cfg.test_dataset.W = H, W
+    assert len(frames) == 3
+    for f in frames:
+        assert f.shape == (48, 48, 3) and f.dtype == np.uint8
+    assert not np.array_equal(frames[0], frames[1])  # the camera moved
