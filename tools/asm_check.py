@@ -19,13 +19,14 @@ KERNELS = ["fwd_kernel<nerf::mlp::PBF16, true, false>", "fwd_kernel<nerf::mlp::P
            "dw_kernel<nerf::mlp::PBF16>", "dw_kernel<nerf::mlp::PF32>"]
 
 
-def build_asm(tmp):
+def build_asm(tmp, kernels=None):
+    kernels = kernels or KERNELS
     src = os.path.join(tmp, "k.hip")
     args = {"fwd": "(nerf::mlp::FwdArgs)", "dx_": "(nerf::mlp::DxArgs)", "dw_": "(nerf::mlp::DwArgs)"}
     with open(src, "w") as f:
         f.write("#define NERF_MLP_DEVICE_ONLY\n")
         f.write(f'#include "{ROOT}/nerf-replication_amd/csrc/mlp.hip"\n')
-        for k in KERNELS:
+        for k in kernels:
             f.write(f"template __global__ void nerf::mlp::{k}{args[k[:3]]};\n")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include",
                     "--cuda-device-only", "-S", src, "-o", os.path.join(tmp, "k.s")], check=True, cwd=tmp)
