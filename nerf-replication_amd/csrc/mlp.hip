@@ -251,8 +251,12 @@ __device__ __forceinline__ void sfor(F&& f) {
 
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 
-constexpr int SLOT_CAP = 72;   // KiB (1 KiB chunks) per ring slot: 2 x 72 KiB of 160 KiB LDS
-constexpr int NSLOT = 2;
+#ifndef NERF_NSLOT
+#define NERF_NSLOT 2
+#endif
+constexpr int NSLOT = NERF_NSLOT;                 // ring slots; DMA runs NSLOT - 1 groups ahead
+constexpr int SLOT_CAP = NSLOT == 2 ? 72 : 48;    // KiB (1 KiB chunks) per slot: <= 144 KiB of 160 KiB LDS
+constexpr int PF = NSLOT - 1;
 constexpr int GROUP_MAX = 8;   // units per group
 #ifndef NERF_GROUP_ACROSS
 #define NERF_GROUP_ACROSS 1    // groups may span layers: every group fills its slot
@@ -324,6 +328,25 @@ __device__ __forceinline__ lds_cu4* lds_ptr(uint32_t byte_addr) {
 // input tile t, chunk c), in execution order.  A group's body is straight-line code over
 // it with the A operand (weights, LDS) prefetched PD steps ahead across unit boundaries
 // -- hipcc on its own keeps one ds_read in flight and waits lgkmcnt(0) before every MFMA.
+// DMA wave-instructions per wave for group g (fetch_group)
+template <class P, int DIR, bool DENSITY>
+__host__ __device__ constexpr int group_dma(int g) {
+  return (GroupTable<DIR, DENSITY, P::CH>::t.g[g].nch + P::WAVES - 1) / P::WAVES;
+}
+// vmcnt of the hand-off at the end of group g (group g + 1's DMA must have landed): the
+// wave's vector-memory ops younger than that DMA = the DMAs of groups g + 2 .. g + PF and
+// the stores of the iterations g + 1 - PF .. g (each issued after its iteration's DMA), plus
+// the prologue's stores when group g + 1 was fetched in the prologue.
+template <class P, int DIR, bool DENSITY, class StoresFn>
+__host__ __device__ constexpr int handoff_vmcnt(int g, StoresFn stores, int prologue_stores) {
+  const int NG = GroupTable<DIR, DENSITY, P::CH>::t.n;
+  int n = 0;
+  for (int j = g + 2; j <= g + PF && j < NG; ++j) n += group_dma<P, DIR, DENSITY>(j);
+  for (int i = (g + 1 - PF > 0 ? g + 1 - PF : 0); i <= g; ++i) n += stores(i);
+  if (g + 1 < PF) n += prologue_stores;
+  return n;
+}
+
 struct Step { int j, u, t, c, off, kin, len; bool first, last; };
 template <int DIR> __host__ __device__ constexpr int unit_tiles(int u) {
   return DIR == 0 ? fwd_unit_tiles(u) : bwd_unit_tiles(u);
@@ -728,11 +751,13 @@ struct FwdWave {
 
   template <int g> __device__ __forceinline__ void step() {
     constexpr int NG = GT::t.n;
-    if constexpr (g + 1 < NG) fetch<g + 1>();
+    if constexpr (g + PF < NG) fetch<g + PF>();
     const uint32_t slot = lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024);
     wb = lds_ptr(slot + (uint32_t)(h * 16));
     group_body<P, 0, DENSITY, g>(*this, lds_ptr(slot + (uint32_t)(lane * 16)));
-    if constexpr (g + 1 < NG) wait_barrier<group_stores(g)>();
+    constexpr int N = handoff_vmcnt<P, 0, DENSITY>(g, [](int i) constexpr { return group_stores(i); },
+                                                   STORE ? 3 * CH : 0);
+    if constexpr (g + 1 < NG) wait_barrier<N>();
   }
 
   __device__ __forceinline__ void run() {
@@ -747,7 +772,7 @@ struct FwdWave {
       dy = a.dirs[di * 3 + 1];
       dz = a.dirs[di * 3 + 2];
     }
-    fetch<0>();
+    sfor<(PF < GT::t.n ? PF : GT::t.n)>([&](auto gg) { fetch<decltype(gg)::value>(); });
     pe_tile<P, 0, 10, 63>(X[0], h, px, py, pz);
     pe_tile<P, 1, 10, 63>(X[1], h, px, py, pz);
     if constexpr (STORE) {
@@ -757,7 +782,14 @@ struct FwdWave {
       store_tile<P>(a.act, a.nblk, AT_TILES, AT_X + 1, wblock, lane, X[1]);
       store_tile<P>(a.act, a.nblk, AT_TILES, AT_D, wblock, lane, Dt);
     }
-    wait_barrier<STORE ? 3 * CH : 0>();
+    {  // group 0 landed: younger = the DMAs of groups 1 .. PF - 1 and the PE stores
+      constexpr int N0 = [] {
+        int n = STORE ? 3 * CH : 0;
+        for (int j = 1; j < PF && j < GT::t.n; ++j) n += group_dma<P, 0, DENSITY>(j);
+        return n;
+      }();
+      wait_barrier<N0>();
+    }
     settle(dx);
     settle(dy);
     settle(dz);
@@ -767,9 +799,19 @@ struct FwdWave {
   }
 };
 
+#ifndef NERF_SETPRIO_YOUNG
+#define NERF_SETPRIO_YOUNG 0
+#endif
+// MI355X_MICROARCH.md "Two waves per SIMD" item 4: waves 4-7 lose VALU arbitration; one
+// static s_setprio 1 for them (wave-uniform condition via readfirstlane)
+__device__ __forceinline__ void young_priority() {
+  if (NERF_SETPRIO_YOUNG && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+}
+
 template <class P, bool STORE, bool DENSITY>
 __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
+  young_priority();
   FwdWave<P, STORE, DENSITY> w(a, smem_u4);
   w.run();
 }
@@ -882,10 +924,11 @@ struct DxWave {
 
   template <int g> __device__ __forceinline__ void step() {
     constexpr int NG = GT::t.n;
-    if constexpr (g + 1 < NG) fetch<g + 1>();
+    if constexpr (g + PF < NG) fetch<g + PF>();
     const uint32_t slot = lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024);
     group_body<P, 1, false, g>(*this, lds_ptr(slot + (uint32_t)(lane * 16)));
-    if constexpr (g + 1 < NG) wait_barrier<group_stores(g)>();
+    constexpr int N = handoff_vmcnt<P, 1, false>(g, [](int i) constexpr { return group_stores(i); }, 2 * CH);
+    if constexpr (g + 1 < NG) wait_barrier<N>();
   }
 
   __device__ __forceinline__ void run() {
@@ -893,7 +936,7 @@ struct DxWave {
     const float4 gr = m < a.M ? *(const float4*)(a.d_raw + m * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < MASK_GROUPS; ++i) mk[i] = *mask_slot((void*)a.masks, wblock, i, lane);
-    fetch<0>();
+    sfor<(PF < GT::t.n ? PF : GT::t.n)>([&](auto gg) { fetch<decltype(gg)::value>(); });
 #pragma unroll
     for (int rho = 0; rho < 16; ++rho) {
       P::set(G, rho, (h == 0 && rho < 3) ? (rho == 0 ? gr.x : rho == 1 ? gr.y : gr.z) : 0.f);
@@ -901,7 +944,14 @@ struct DxWave {
     }
     store_tile<P>(a.dz, a.nblk, ZT_TILES, ZT_RGB, wblock, lane, G);
     store_tile<P>(a.dz, a.nblk, ZT_TILES, ZT_A, wblock, lane, DA);
-    wait_barrier<2 * CH>();
+    {
+      constexpr int N0 = [] {
+        int n = 2 * CH;
+        for (int j = 1; j < PF && j < GT::t.n; ++j) n += group_dma<P, 1, false>(j);
+        return n;
+      }();
+      wait_barrier<N0>();
+    }
 #pragma unroll
     for (int i = 0; i < MASK_GROUPS; ++i) {
       settle(mk[i].x);
@@ -916,6 +966,7 @@ struct DxWave {
 template <class P>
 __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
+  young_priority();
   DxWave<P> w(a, smem_u4);
   w.run();
 }

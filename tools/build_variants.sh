@@ -12,7 +12,7 @@ while [ $# -gt 1 ]; do
   (
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$ROOT/include $defs -c ${SRC:-$CS/mlp.hip} -o /tmp/var_$name.o &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/variants/$name.so /tmp/var_$name.o \
-      $ROOT/build/nerf_amd/sampling.hip.o $ROOT/build/nerf_amd/grid.hip.o $ROOT/build/nerf_amd/optim.hip.o $ROOT/build/nerf_amd/errors.cpp.o
+      $ROOT/build/nerf_amd/sampling.hip.o $ROOT/build/nerf_amd/grid.hip.o $ROOT/build/nerf_amd/optim.hip.o $ROOT/build/nerf_amd/metrics.hip.o $ROOT/build/nerf_amd/errors.cpp.o
   ) &
   pids+=($!)
 done
