@@ -39,6 +39,8 @@ STORE_ROWS = (79 + 78) * 32
 BOUND = {"mlp_fwd_train": "mfma", "mlp_fwd": "mfma", "mlp_bwd_dx": "mfma", "mlp_bwd_dw": "hbm"}
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+# HBM-bound sampling / compositing kernels; ops.py counts their algorithmic bytes per launch
+STREAM_KERNELS = ("raygen", "sample_stratified", "sample_pdf", "composite_fwd", "composite_bwd")
 
 
 def parse():
@@ -53,6 +55,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-render", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=1024)
+    ap.add_argument("--detail-steps", type=int, default=5,
+                    help="extra untimed steps that time the sampling/compositing kernels (after the timed region)")
     return ap.parse_args()
 
 
@@ -110,6 +114,36 @@ def train_step(cfg, trainer, opt, ds, device):
     return trainer.train_step(batch, opt)
 
 
+def stream_roofline(ktimes, dtype=None):
+    """{kernel: launches, avg_ms, achieved GB/s of algorithmic bytes, frac of HBM peak} for the
+    HBM-bound sampling and compositing kernels (HIP events on the launching stream).  With
+    ``dtype`` (training-step sizes, which the PMC passes run) the PMC traffic per launch is added."""
+    out = {}
+    for k in STREAM_KERNELS:
+        if k not in ktimes:
+            continue
+        n, ms, nbytes = ktimes[k]
+        ach = nbytes / (ms * 1e-3) / 1e9
+        out[k] = {"launches": n, "avg_ms": round(ms / n, 4), "bytes_per_launch": nbytes // n, "bound": "hbm",
+                  "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4)}
+        if dtype is not None:
+            out[k]["traffic"] = pmc_traffic(k, dtype)[0]
+    return out
+
+
+def detail_times(fn, dtype=None):
+    from nerf_amd import ops
+    torch.cuda.synchronize()
+    ops.KERNEL_TIMES.reset()
+    ops.KERNEL_TIMES.enabled = ops.KERNEL_TIMES.detail = True
+    try:
+        fn()
+        torch.cuda.synchronize()
+    finally:
+        ops.KERNEL_TIMES.enabled = ops.KERNEL_TIMES.detail = False
+    return stream_roofline(ops.KERNEL_TIMES.summary(), dtype)
+
+
 def render_frame_time(cfg, net, ds, device, reps=2):
     from src.models.nerf.renderer.volume_renderer import Renderer
     r = Renderer(net)
@@ -127,9 +161,11 @@ def render_frame_time(cfg, net, ds, device, reps=2):
             r.render(batch)
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t0)
+        # one more frame with the sampling / compositing kernels timed (outside the timed reps)
+        stream = detail_times(lambda: r.render(batch))
     net.train()
     cfg.task_arg.perturb = perturb
-    return min(times)
+    return min(times), stream
 
 
 def grid_times(cfg, net, ds, device, reps=2):
@@ -230,7 +266,11 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
-    ktimes = ops.KERNEL_TIMES.summary()
+    ktimes = {k: v for k, v in ops.KERNEL_TIMES.summary().items() if k not in STREAM_KERNELS}
+    # sampling / compositing kernels per launch, in extra steps after the timed region
+    train_stream = detail_times(lambda: [train_step(cfg, trainer, opt, ds, device) for _ in range(args.detail_steps)],
+                                 args.dtype) \
+        if args.detail_steps > 0 else {}
 
     rays_total = world * args.rays * args.steps
     value = rays_total / elapsed
@@ -260,9 +300,9 @@ def main():
               "roofline": roof(k, n, m, u)}
           for k, (n, m, u) in ktimes.items()}
 
-    render_s, grid = None, None
+    render_s, grid, render_stream = None, None, None
     if rank == 0 and not args.no_render and world == 1:
-        render_s = render_frame_time(cfg, net, ds, device)
+        render_s, render_stream = render_frame_time(cfg, net, ds, device)
         grid = grid_times(cfg, net, ds, device)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -280,6 +320,7 @@ def main():
                        "samples_per_ray": 64 + 192, "parallelism": f"dp{world}"},
             "roofline": roofline,
             "kernels": kt,
+            "stream_kernels": {"train_step": train_stream, "render_800x800": render_stream},
             "render_s_per_frame": None if render_s is None else round(render_s, 4),
             "occupancy_grid": grid,
             "cpu_baseline": cpu,

@@ -88,8 +88,13 @@ def _scalar_dev(x, device) -> torch.Tensor:
 # optional per-kernel timing with HIP events on the launching stream (bench.py roofline)
 # --------------------------------------------------------------------------------------
 class _KernelTimes:
+    """MLP kernels are timed whenever ``enabled``; the HBM-bound sampling / compositing kernels
+    (units = algorithmic bytes) only when ``detail`` is also set, so that a
+    headline timing run carries no extra events on those short launches."""
+
     def __init__(self):
         self.enabled = False
+        self.detail = False
         self.pending = []  # (name, units, start_event, end_event)
 
     def reset(self):
@@ -108,18 +113,19 @@ KERNEL_TIMES = _KernelTimes()
 
 
 class kernel_timer:
-    def __init__(self, name, units):
+    def __init__(self, name, units, detail=False):
         self.name, self.units = name, units
+        self.on = KERNEL_TIMES.enabled and (KERNEL_TIMES.detail or not detail)
 
     def __enter__(self):
-        if KERNEL_TIMES.enabled:
+        if self.on:
             self.a = torch.cuda.Event(enable_timing=True)
             self.b = torch.cuda.Event(enable_timing=True)
             self.a.record(torch.cuda.current_stream())
         return self
 
     def __exit__(self, *exc):
-        if KERNEL_TIMES.enabled:
+        if self.on:
             self.b.record(torch.cuda.current_stream())
             KERNEL_TIMES.pending.append((self.name, self.units, self.a, self.b))
         return False
@@ -143,8 +149,11 @@ def raygen(c2w: torch.Tensor, H: int, W: int, focal: float, pix: Optional[torch.
     pout = torch.empty(R, device=dev, dtype=torch.int64) if want_pix else None
     if images is not None:
         images = _f32c(images, "images")
-    check(lib().nerf_raygen(ptr(c2w), c2w.shape[0], H, W, float(focal), ptr(pix), R, seed, offset, ptr(images),
-                            ptr(rays), ptr(rgb), ptr(pout), stream_of(c2w)), "nerf_raygen")
+    # bytes per ray: pixel id read (given) or written (want_pix), 24 B rays, 12 B rgb gather + 12 B write
+    nbytes = R * (24 + (8 if pix is not None else 0) + (8 if want_pix else 0) + (24 if images is not None else 0))
+    with kernel_timer("raygen", nbytes, detail=True):
+        check(lib().nerf_raygen(ptr(c2w), c2w.shape[0], H, W, float(focal), ptr(pix), R, seed, offset, ptr(images),
+                                ptr(rays), ptr(rgb), ptr(pout), stream_of(c2w)), "nerf_raygen")
     return rays, rgb, pout
 
 
@@ -161,9 +170,12 @@ def sample_stratified(rays: torch.Tensor, near, far, n_samples: int, perturb: bo
     if t_rand is not None:
         t_rand = _f32c(t_rand, "t_rand")
     near_t, far_t = _scalar_dev(near, dev), _scalar_dev(far, dev)  # keep alive across the launch
-    check(lib().nerf_sample_stratified(ptr(rays), R, n_samples, ptr(t_lin), ptr(near_t), ptr(far_t),
-                                       int(bool(perturb)), ptr(t_rand), seed, offset, ptr(z), ptr(pts), ptr(vd),
-                                       stream_of(rays)), "nerf_sample_stratified")
+    # bytes per ray: 24 B ray read, 4 B z (+12 B pts, +4 B injected uniform) per sample, 12 B viewdir
+    nbytes = R * (24 + 12 + n_samples * (4 + (12 if want_pts else 0) + (4 if t_rand is not None else 0)))
+    with kernel_timer("sample_stratified", nbytes, detail=True):
+        check(lib().nerf_sample_stratified(ptr(rays), R, n_samples, ptr(t_lin), ptr(near_t), ptr(far_t),
+                                           int(bool(perturb)), ptr(t_rand), seed, offset, ptr(z), ptr(pts), ptr(vd),
+                                           stream_of(rays)), "nerf_sample_stratified")
     return z, pts, vd
 
 
@@ -199,10 +211,14 @@ def sample_pdf(z: torch.Tensor, weights: torch.Tensor, n_importance: int, det: b
     u_lin = device_table("linspace", 0.0, 1.0, n_importance, dev) if det else None
     if u is not None:
         u = _f32c(u, "u")
-    check(lib().nerf_sample_pdf(ptr(z), ptr(weights), R, Sc, n_importance, int(bool(det)), ptr(u_lin), ptr(u), seed,
-                                offset, ptr(rays), ptr(out["z_fine"]), ptr(out.get("pts_fine")),
-                                ptr(out.get("samples")), ptr(out.get("cdf")), ptr(out.get("inds")), stream_of(z)),
-          "nerf_sample_pdf")
+    # bytes per ray: z + weights read (8 B per coarse sample), injected u, ray; merged z (+ pts) written
+    nbytes = R * (8 * Sc + (4 * n_importance if u is not None else 0) + (24 if rays is not None else 0)
+                  + S * (4 + (12 if rays is not None else 0)) + (12 * n_importance + 4 * (Sc - 1) if debug else 0))
+    with kernel_timer("sample_pdf", nbytes, detail=True):
+        check(lib().nerf_sample_pdf(ptr(z), ptr(weights), R, Sc, n_importance, int(bool(det)), ptr(u_lin), ptr(u),
+                                    seed, offset, ptr(rays), ptr(out["z_fine"]), ptr(out.get("pts_fine")),
+                                    ptr(out.get("samples")), ptr(out.get("cdf")), ptr(out.get("inds")), stream_of(z)),
+              "nerf_sample_pdf")
     return out
 
 
@@ -247,8 +263,10 @@ class _Composite(torch.autograd.Function):
         depth = torch.empty(R, device=dev, dtype=torch.float32)
         acc = torch.empty(R, device=dev, dtype=torch.float32)
         w = torch.empty(R, S, device=dev, dtype=torch.float32)
-        check(lib().nerf_composite_fwd(ptr(raw), ptr(z), dptr, dstride, R, S, int(bool(white)), ptr(rgb), ptr(depth),
-                                       ptr(acc), ptr(w), stream_of(raw)), "nerf_composite_fwd")
+        # bytes per ray: raw 16 B + z 4 B read and weight 4 B written per sample; dir 12 B; rgb/depth/acc 20 B
+        with kernel_timer("composite_fwd", R * (24 * S + 32), detail=True):
+            check(lib().nerf_composite_fwd(ptr(raw), ptr(z), dptr, dstride, R, S, int(bool(white)), ptr(rgb),
+                                           ptr(depth), ptr(acc), ptr(w), stream_of(raw)), "nerf_composite_fwd")
         ctx.set_materialize_grads(False)  # unused outputs (depth, acc) arrive as None, not zero-filled
         ctx.save_for_backward(raw, z, keep)
         ctx.dptr, ctx.dstride, ctx.white = dptr, dstride, int(bool(white))
@@ -267,8 +285,11 @@ class _Composite(torch.autograd.Function):
         g_depth = None if g_depth is None else g_depth.contiguous()
         g_acc = None if g_acc is None else g_acc.contiguous()
         g_raw = torch.empty_like(raw)
-        check(lib().nerf_composite_bwd(ptr(raw), ptr(z), ctx.dptr, ctx.dstride, R, S, ctx.white, ptr(g_rgb),
-                                       ptr(g_depth), ptr(g_acc), ptr(g_raw), stream_of(raw)), "nerf_composite_bwd")
+        # bytes per ray: raw 16 B + z 4 B read and d_raw 16 B written per sample; dir 12 B; output grads
+        nbytes = R * (36 * S + 24 + (4 if g_depth is not None else 0) + (4 if g_acc is not None else 0))
+        with kernel_timer("composite_bwd", nbytes, detail=True):
+            check(lib().nerf_composite_bwd(ptr(raw), ptr(z), ctx.dptr, ctx.dstride, R, S, ctx.white, ptr(g_rgb),
+                                           ptr(g_depth), ptr(g_acc), ptr(g_raw), stream_of(raw)), "nerf_composite_bwd")
         return g_raw, None, None, None
 
 

@@ -1,4 +1,4 @@
-"""Per-launch HBM traffic of the MLP kernels from rocprofv3 --pmc CSVs.
+"""Per-launch HBM traffic of the MLP, sampling and compositing kernels from rocprofv3 --pmc CSVs.
 
     rocprofv3 --pmc FETCH_SIZE -d <dir_f> -o fetch --output-format csv -- python3 bench.py ...
     rocprofv3 --pmc WRITE_SIZE -d <dir_w> -o write --output-format csv -- python3 bench.py ...
@@ -22,6 +22,13 @@ LABELS = {
     "dx_kernel<nerf::mlp::PF32>": "mlp_bwd_dx",
     "dw_kernel<nerf::mlp::PBF16>": "mlp_bwd_dw",
     "dw_kernel<nerf::mlp::PF32>": "mlp_bwd_dw",
+    "raygen_kernel(": "raygen",
+    "stratified_kernel(": "sample_stratified",
+    "sample_pdf_kernel(": "sample_pdf",
+    "composite_kernel<1, false>": "composite_fwd",
+    "composite_kernel<3, false>": "composite_fwd",
+    "composite_kernel<1, true>": "composite_bwd",
+    "composite_kernel<3, true>": "composite_bwd",
 }
 
 
