@@ -1,0 +1,179 @@
+"""GPU parity at BASELINE.json's full sizes, through size-independent properties.
+
+The oracle finishes a few hundred rays in seconds, so the full sizes (a 4096-ray training batch,
+config 3; all 640,000 rays of an 800x800 view, configs 2/4) are checked by properties that do not
+depend on the batch:
+- row independence: every ray's outputs in the full batch are bit-identical to the same rays run
+  alone (sampling, importance sampling + merge, compositing, and the whole bf16 render);
+- structure: stratified and merged depths sorted and inside [near, far], the merged depths contain
+  the coarse depths, points = o + d*z as the reference rounds them, weights >= 0, acc in [0, 1];
+- a sampled subset of the full frame against the oracle, at the bf16 tolerance of
+  test_gpu_render.test_render_perturb0 (north_star: rgb/depth 2e-3, depth scaled by its range 6),
+  leaving out the few rays on the reference's last-sample discontinuity (see the test).
+Empty (R = 0) and ragged (R not a multiple of the wave / block size) batches are covered too.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+os.environ.setdefault("NERF_AMD_NO_ARGV", "1")
+
+H = W = 800
+CAM_X = 0.6911112070083618  # lego camera_angle_x (blender.py:74-75)
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import nerf_oracle
+    return nerf_oracle
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from nerf_amd import ops
+    return ops
+
+
+@pytest.fixture(scope="module")
+def frame_rays(cuda, ops, O):
+    """All rays of the 800x800 view at theta=30 (render_video.py:14-19 pose), device [640000, 6]."""
+    pose = O.pose_spherical(30.0, -30.0, 4.0).to(cuda)
+    pix = torch.arange(H * W, device=cuda)
+    rays, _, _ = ops.raygen(pose[None], H, W, O.focal_from_angle(W, CAM_X), pix=pix)
+    return rays
+
+
+def _subset(n, hi, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randperm(hi, generator=g)[:n].sort().values
+
+
+def test_training_batch_sampling_properties(cuda, ops, frame_rays):
+    R = 4096
+    idx = _subset(R, frame_rays.shape[0], 0).to(cuda)
+    rays = frame_rays[idx].contiguous()
+    z, pts, vd = ops.sample_stratified(rays, 2.0, 6.0, 64, True, seed=7, offset=3)
+    zc = z.cpu()
+    assert torch.all(zc[:, 1:] >= zc[:, :-1]) and float(zc.min()) >= 2.0 and float(zc.max()) <= 6.0
+    ref_pts = rays[:, None, :3] + rays[:, None, 3:] * z[..., None]  # two kernels: no FMA contraction
+    assert torch.equal(pts, ref_pts)
+    # the same rays alone give the same jittered depths (Philox keyed by ray index + offset)
+    z1, pts1, _ = ops.sample_stratified(rays[:1000], 2.0, 6.0, 64, True, seed=7, offset=3)
+    assert torch.equal(z1, z[:1000]) and torch.equal(pts1, pts[:1000])
+
+    # coarse weights from a smooth synthetic density, then importance sampling + merge
+    g = torch.Generator(device=cuda).manual_seed(11)
+    raw = torch.randn(R, 64, 4, device=cuda, generator=g)
+    raw[..., 3] = raw[..., 3].abs() * 3.0
+    rgb, depth, acc, w = ops.composite(raw, z, rays[:, 3:], True)
+    for det in (True, False):
+        out = ops.sample_pdf(z, w, 128, det, seed=5, offset=1, rays=rays)
+        zf = out["z_fine"].cpu()
+        assert zf.shape == (R, 192)
+        assert torch.all(zf[:, 1:] >= zf[:, :-1]) and float(zf.min()) >= 2.0 and float(zf.max()) <= 6.0
+        # the merged row holds every coarse depth (merge, not resample)
+        for r in range(0, R, 97):
+            assert np.isin(zc[r].numpy(), zf[r].numpy()).all(), r
+        ref_pf = rays[:, None, :3] + rays[:, None, 3:] * out["z_fine"][..., None]
+        assert torch.equal(out["pts_fine"], ref_pf)
+        alone = ops.sample_pdf(z[:333], w[:333], 128, det, seed=5, offset=1, rays=rays[:333])
+        assert torch.equal(alone["z_fine"], out["z_fine"][:333])
+
+
+def test_composite_full_frame_properties(cuda, ops, frame_rays):
+    R, S = frame_rays.shape[0], 192
+    g = torch.Generator(device=cuda).manual_seed(3)
+    z = torch.sort(torch.rand(R, S, device=cuda, generator=g) * 4 + 2, -1).values
+    raw = torch.randn(R, S, 4, device=cuda, generator=g)
+    rgb, depth, acc, w = ops.composite(raw, z, frame_rays[:, 3:], True)
+    assert float(w.min()) >= 0.0
+    assert float(acc.min()) >= 0.0 and float(acc.max()) <= 1.0 + 1e-6
+    assert float(rgb.min()) >= 0.0 and float(rgb.max()) <= 1.0 + 1e-6
+    np.testing.assert_allclose(w.sum(-1).cpu().numpy(), acc.cpu().numpy(), rtol=0, atol=2e-5)
+    idx = _subset(4099, R, 1).to(cuda)  # ragged
+    r2, d2, a2, w2 = ops.composite(raw[idx], z[idx], frame_rays[idx, 3:], True)
+    assert torch.equal(r2, rgb[idx]) and torch.equal(d2, depth[idx]) and torch.equal(a2, acc[idx])
+    assert torch.equal(w2, w[idx])
+
+
+def test_empty_batches(cuda, ops):
+    rays = torch.zeros(0, 6, device=cuda)
+    z, pts, vd = ops.sample_stratified(rays, 2.0, 6.0, 64, False)
+    assert z.shape == (0, 64) and pts.shape == (0, 64, 3) and vd.shape == (0, 3)
+    rgb, depth, acc, w = ops.composite(torch.zeros(0, 64, 4, device=cuda), z, rays[:, 3:], True)
+    assert rgb.shape == (0, 3) and depth.shape == (0,) and w.shape == (0, 64)
+    out = ops.sample_pdf(z, w, 128, True, rays=rays)
+    assert out["z_fine"].shape == (0, 192) and out["pts_fine"].shape == (0, 192, 3)
+
+
+def test_full_frame_render_row_independent_and_matches_oracle(cuda, ops, O, seeded_state, frame_rays):
+    """One 800x800 view (640,000 rays, 262,144-ray render chunks) through the drop-in Renderer with
+    the bf16 MLP: a ragged subset rendered alone is bit-identical to the same rays in the frame,
+    and 48 rays of the frame agree with the oracle (fp32 reference restatement)."""
+    from src.config import cfg
+    from src.models.nerf.network import Network
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    saved = (cfg.task_arg.mlp_dtype, cfg.task_arg.perturb)
+    cfg.task_arg.mlp_dtype = "bf16"
+    cfg.task_arg.perturb = 0
+    try:
+        _render_checks(cfg, cuda, O, seeded_state, frame_rays, Network, Renderer)
+    finally:
+        cfg.task_arg.mlp_dtype, cfg.task_arg.perturb = saved
+
+
+def _render_checks(cfg, cuda, O, seeded_state, frame_rays, Network, Renderer):
+    torch.manual_seed(0)
+    net = Network().to(cuda)
+    net.mlp_dtype = "bf16"
+    net.eval()
+    r = Renderer(net)
+    near, far = torch.tensor([2.0], device=cuda), torch.tensor([6.0], device=cuda)
+    keys = ["rgb_map_c", "depth_map_c", "acc_map_c", "rgb_map_f", "depth_map_f", "acc_map_f"]
+    with torch.no_grad():
+        full = r.render({"rays": frame_rays[None], "near": near, "far": far})
+        for k in keys:
+            assert full[k].shape[0] == H * W, k
+            assert torch.isfinite(full[k]).all(), k
+        assert float(full["acc_map_f"].min()) >= 0.0 and float(full["acc_map_f"].max()) <= 1.0 + 1e-5
+        idx = _subset(1001, H * W, 2).to(cuda)
+        part = r.render({"rays": frame_rays[idx][None], "near": near, "far": far})
+    for k in keys:
+        assert torch.equal(part[k], full[k][idx]), k
+
+    C, Fn = O.split_params(seeded_state, "model"), O.split_params(seeded_state, "model_fine")
+    sub = _subset(96, H * W, 3)
+    with torch.no_grad():
+        ref = O.render(C, Fn, frame_rays[sub.to(cuda)].cpu(), torch.tensor([2.0]), torch.tensor([6.0]), keep=True)
+    # The reference's last interval is 1e10 long (volume_renderer.py:42): the last sample's alpha
+    # jumps from 0 to 1 as sigma = ReLU(raw[3]) leaves 0, so a ray whose last pre-activation
+    # changes sign between the fp32 reference and the bf16 MLP takes the last sample's colour
+    # instead of the white background.  That is a discontinuity of the reference, not a
+    # tolerance question.  Such rays are found exactly, from this MLP's own raw at the last sample
+    # (z = far for both passes, since the merge keeps the coarse depths), counted, and left out
+    # of the tolerance check.  The coarse weights passed to sample_pdf exclude the last sample
+    # (volume_renderer.py:214), so a coarse flip does not reach the fine pass.
+    rs = frame_rays[sub.to(cuda)]
+    last = (rs[:, :3] + rs[:, 3:] * 6.0)[:, None, :]
+    vd = rs[:, 3:] / torch.norm(rs[:, 3:], dim=-1, keepdim=True)
+    with torch.no_grad():
+        ours = {"c": net(last, vd, "")[:, 0, 3].cpu(), "f": net(last, vd, "fine")[:, 0, 3].cpu()}
+    unstable = {p: (ours[p] > 0) != (ref[f"raw_{p}"][:, -1, 3] > 0) for p in "cf"}
+    assert int(unstable["c"].sum()) + int(unstable["f"].sum()) <= len(sub) // 8, unstable
+    for k in keys:
+        keep = ~unstable[k[-1]]
+        tol = 2e-3 * (6.0 if "depth" in k else 1.0)
+        got, want = full[k][sub.to(cuda)].cpu()[keep].numpy(), ref[k][keep].numpy()
+        if k.endswith("_f"):
+            # end to end the fine pass sees the CDF of bf16 coarse weights, so a few importance
+            # samples move to a neighbouring bin (see test_gpu_render.E2E_FINE_DEPTH_TOL for the
+            # fp32 case); given the same samples the fine pass is held to the plain tolerance
+            # (test_gpu_render.test_fine_pass_given_reference_samples).  Here: 95 % of the rays
+            # within the plain tolerance, all within twice it.
+            assert np.mean(np.abs(got - want) <= tol) >= 0.95, (k, np.abs(got - want).max())
+            tol *= 2
+        np.testing.assert_allclose(got, want, rtol=0, atol=tol, err_msg=f"{k}: rays {sub[keep].tolist()}")
