@@ -11,10 +11,18 @@ MLP -> compositing -> MSE(c)+MSE(f) -> backward of everything -> gradient all-re
 (RCCL, N > 1) -> fused clip_grad_value_(40) + Adam.  Weak scaling: 4096 rays per GPU.
 Weights: the reference's seed-0 init (torch.manual_seed(0); Network()).  Data is
 synthetic (no dataset offline).  Rank 0 prints one JSON line.
+
+The headline (``value``, ``dtype`` "fp32") runs the MLP in fp32 MFMA, the reference's own
+precision (nn.Linear fp32, network.py:22-74).  The opt-in bf16 MLP (north_star: rgb/depth
+within 2e-3) is measured in the same run and reported as the nested, labelled ``bf16_line``.
+``vs_baseline`` divides by the reference's per-step op graph run eagerly by PyTorch-ROCm on
+the same GPU at the same MLP dtype and perturb (``baseline``); ``cpu_baseline`` is the same
+graph on the host cores (config 1).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -29,14 +37,15 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "train rays/sec (fwd+bwd, 64+128 samples) + 800x800 render s/frame, 1/2/4/8 GPU"
 # algorithmic FLOP per MLP sample: 593,408 MAC forward; backward dX 557,696 MAC
-# (no input grad for PE(xyz) at layers 0/5 and PE(dir) at the view layer), dW 593,408 MAC
+# (no input grad for PE(xyz) at layers 0/5 and PE(dir) at the view layer), dW 593,408 MAC.
+# Every MLP kernel is priced against the MFMA peak of its dtype (SURVEY.md 8d roofline table).
 FLOP_PER_SAMPLE = {"mlp_fwd_train": 2 * 593408, "mlp_fwd": 2 * 593408, "mlp_bwd_dx": 2 * 557696,
                    "mlp_bwd_dw": 2 * 593408}
-# the dW GEMMs stream the training stores once: every stored activation tile (79 x 32 rows)
-# and output-gradient tile (78 x 32 rows) of a sample, 2 B (bf16) / 4 B (fp32) per value
-# (DESIGN.md 4); that makes dW HBM-bound, the other MLP kernels MFMA-bound
+# bytes the training stores add per sample: 79 activation + 78 output-gradient
+# tiles of 32 rows, written once and read once; the MLP's own algorithmic I/O is 44 B/sample
+# (pts 12 + raw 16 + d_raw 16)
 STORE_ROWS = (79 + 78) * 32
-BOUND = {"mlp_fwd_train": "mfma", "mlp_fwd": "mfma", "mlp_bwd_dx": "mfma", "mlp_bwd_dw": "hbm"}
+MLP_IO_BYTES = 12 + 16 + 16
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
 # HBM-bound sampling / compositing kernels; ops.py counts their algorithmic bytes per launch
@@ -49,10 +58,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU per step")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"], help="headline MLP dtype")
     ap.add_argument("--images", type=int, default=100)
     ap.add_argument("--res", type=int, default=800)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-eager-baseline", action="store_true")
+    ap.add_argument("--no-second", action="store_true", help="skip the labelled bf16 (or fp32) second line")
     ap.add_argument("--no-render", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=1024)
     ap.add_argument("--detail-steps", type=int, default=5,
@@ -63,9 +74,9 @@ def parse():
 def pmc_traffic(kernel, dtype):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/r*/traffic.json, written by tools/pmc_traffic.py from rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+    FETCH_SIZE / WRITE_SIZE passes of this bench), or (None, None)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic*.json")), reverse=True):
         with open(path) as f:
             d = json.load(f)
         if d.get("dtype") == dtype and kernel in d.get("kernels", {}):
@@ -83,9 +94,9 @@ def setup_dist():
     return world, rank, torch.device("cuda", local)
 
 
-def build(args, device):
+def build(args, device, dtype):
     from src.config import cfg
-    cfg.task_arg.mlp_dtype = args.dtype
+    cfg.task_arg.mlp_dtype = dtype
     cfg.task_arg.train_rays = args.rays
     cfg.task_arg.perturb = 1
     from src.datasets.nerf.blender import Dataset
@@ -144,109 +155,23 @@ def detail_times(fn, dtype=None):
     return stream_roofline(ops.KERNEL_TIMES.summary(), dtype)
 
 
-def render_frame_time(cfg, net, ds, device, reps=2):
-    from src.models.nerf.renderer.volume_renderer import Renderer
-    r = Renderer(net)
-    perturb = cfg.task_arg.perturb
-    cfg.task_arg.perturb = 0
-    rays, _ = ds.image_rays(0)
-    batch = {"rays": rays, "near": torch.tensor([2.0], device=device), "far": torch.tensor([6.0], device=device)}
-    net.eval()
-    times = []
-    with torch.no_grad():
-        r.render(batch)
-        for _ in range(reps):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            r.render(batch)
-            torch.cuda.synchronize()
-            times.append(time.perf_counter() - t0)
-        # one more frame with the sampling / compositing kernels timed (outside the timed reps)
-        stream = detail_times(lambda: r.render(batch))
-    net.train()
-    cfg.task_arg.perturb = perturb
-    return min(times), stream
+def mlp_roofline(k, n, ms, units, dtype):
+    """Algorithmic FLOP of one launch (SURVEY.md 8d per-sample figure x samples) / its mean
+    HIP-event duration, against the dtype's dense MFMA peak."""
+    avg_ms = ms / n
+    per = FLOP_PER_SAMPLE[k] * units / n
+    ach = per / (avg_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s",
+            "frac": round(ach / PEAK_TFLOPS[dtype], 4), "flop_per_launch": per, "samples_per_launch": units // n,
+            "avg_launch_ms": round(avg_ms, 4)}
 
 
-def grid_times(cfg, net, ds, device, reps=2):
-    """BASELINE config 4: the 128^3 x 8-corner occupancy bake (occupancy_grid.py:15-80) and the
-    grid-accelerated 800x800 march (render_accelerated, volume_renderer.py:268-357) of test
-    view 0 through the reference's own baked lego grid (tests/golden/lego_occupancy_grid.npz,
-    packed bits of logs/lego/occupancy_grid.pt).  Weights are the synthetic seed-0 init."""
-    import numpy as np
+def measure_training(args, world, rank, device, dtype):
+    """Warmup + exactly args.steps timed steps (barrier + synchronize on both sides, max over
+    ranks).  Returns (rays/s, ms/step, roofline, per-kernel table, train-size stream kernels,
+    (cfg, net, ds))."""
     from nerf_amd import ops
-    from src.models.nerf.renderer.volume_renderer import Renderer
-    out = {}
-    with torch.no_grad():
-        def bake():
-            return ops.bake(net.model.packer(), 128, 1.0, dtype=cfg.task_arg.mlp_dtype)
-        bake()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            grid = bake()
-        torch.cuda.synchronize()
-        out["bake_s"] = round((time.perf_counter() - t0) / reps, 4)
-        out["bake_occupied"] = int(grid.sum())
-        z = np.load(os.path.join(ROOT, "tests", "golden", "lego_occupancy_grid.npz"), allow_pickle=False)
-        shape = tuple(int(v) for v in z["shape"])
-        lego = torch.from_numpy(np.unpackbits(z["packed"])[: int(np.prod(shape))].reshape(shape).astype(bool))
-        r = Renderer(net)
-        r.set_occupancy_grid(lego, device)
-        rays, _ = ds.image_rays(0)
-        batch = {"rays": rays, "near": ops.device_scalar(2.0, device), "far": ops.device_scalar(6.0, device)}
-        import contextlib
-        import io
-        with contextlib.redirect_stdout(io.StringIO()):
-            r.render_accelerated(batch)
-            times = []
-            for _ in range(reps):
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                o = r.render_accelerated(batch)
-                torch.cuda.synchronize()
-                times.append(time.perf_counter() - t0)
-        out["march_s_per_frame"] = round(min(times), 4)
-        out["march_queried_points"] = int(o["n_queried"])
-    return out
-
-
-def cpu_baseline(n_rays):
-    """The oracle (tests-only CPU restatement of the reference, torch CPU) on a bounded
-    sample: one n_rays forward+backward render (perturb 0), config 1 of BASELINE.json."""
-    from oracle import nerf_oracle as O
-    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
-    state = {k: v.clone().requires_grad_(True) for k, v in O.seeded_network_state(0).items()}
-    C, Fn = O.split_params(state, "model"), O.split_params(state, "model_fine")
-    pose = O.pose_spherical(30.0, -30.0, 4.0)
-    o, d = O.get_rays(800, 800, O.focal_from_angle(800, 0.6911112070083618), pose)
-    idx = torch.randint(0, 800 * 800, (n_rays,), generator=torch.Generator().manual_seed(0))
-    rays = torch.cat([o.reshape(-1, 3)[idx], d.reshape(-1, 3)[idx]], 1)
-    gt = torch.rand(n_rays, 3, generator=torch.Generator().manual_seed(1))
-
-    def once():
-        for v in state.values():
-            v.grad = None
-        ret = O.render(C, Fn, rays, torch.tensor([2.0]), torch.tensor([6.0]))
-        O.loss_fn(ret, gt)[0].backward()
-
-    once()
-    t0 = time.perf_counter()
-    reps = 5
-    for _ in range(reps):
-        once()
-    dt = (time.perf_counter() - t0) / reps
-    return {"value": round(n_rays / dt, 2), "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{n_rays}-ray forward+backward render (64+128 samples, perturb 0, seed-0 weights), "
-                      f"mean of {reps} after 1 warm-up, torch {torch.__version__} CPU"}
-
-
-def main():
-    args = parse()
-    world, rank, device = setup_dist()
-    from nerf_amd import ops
-    cfg, net, trainer, opt, ds = build(args, device)
-
+    cfg, net, trainer, opt, ds = build(args, device, dtype)
     for _ in range(args.warmup):
         train_step(cfg, trainer, opt, ds, device)
     if world > 1:
@@ -267,64 +192,294 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     ktimes = {k: v for k, v in ops.KERNEL_TIMES.summary().items() if k not in STREAM_KERNELS}
-    # sampling / compositing kernels per launch, in extra steps after the timed region
     train_stream = detail_times(lambda: [train_step(cfg, trainer, opt, ds, device) for _ in range(args.detail_steps)],
-                                 args.dtype) \
-        if args.detail_steps > 0 else {}
-
-    rays_total = world * args.rays * args.steps
-    value = rays_total / elapsed
-    # dominant kernel: largest total device time among the MLP kernels, priced against the
-    # roofline that bounds it
-    esize = 2 if args.dtype == "bf16" else 4
-
-    def roof(k, n, ms, units):
-        avg_ms = ms / n
-        if BOUND[k] == "hbm":
-            per = STORE_ROWS * esize * units / n
-            ach = per / (avg_ms * 1e-3) / 1e9
-            return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(ach / PEAK_HBM_GBS, 4), "bytes_per_launch": per, "avg_launch_ms": round(avg_ms, 4)}
-        per = FLOP_PER_SAMPLE[k] * units / n
-        ach = per / (avg_ms * 1e-3) / 1e12
-        return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s",
-                "frac": round(ach / PEAK_TFLOPS[args.dtype], 4), "flop_per_launch": per,
-                "avg_launch_ms": round(avg_ms, 4)}
-
+                                dtype) if args.detail_steps > 0 else {}
+    value = world * args.rays * args.steps / elapsed
+    # dominant kernel: largest total device time among the MLP kernels
     name, (n_launch, ms, units) = max(ktimes.items(), key=lambda kv: kv[1][1])
-    traffic, traffic_src = pmc_traffic(name, args.dtype)
-    roofline = dict(kernel=name, **roof(name, n_launch, ms, units), traffic=traffic,
-                    traffic_unit="HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)", traffic_source=traffic_src)
-    kt = {k: {"launches": n, "avg_ms": round(m / n, 4), "samples_per_launch": u // n,
-              "tflops": round(FLOP_PER_SAMPLE.get(k, 0) * (u / n) / (m / n * 1e-3) / 1e12, 2),
-              "roofline": roof(k, n, m, u)}
+    esize = 2 if dtype == "bf16" else 4
+    traffic, traffic_src = pmc_traffic(name, dtype)
+    store_bytes = STORE_ROWS * esize * units / n_launch
+    io_bytes = MLP_IO_BYTES * units / n_launch
+    roofline = dict(kernel=name, **mlp_roofline(name, n_launch, ms, units, dtype), traffic=traffic,
+                    traffic_unit="HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)", traffic_source=traffic_src,
+                    store_bytes_per_launch=store_bytes, mlp_io_bytes_per_launch=io_bytes,
+                    traffic_vs_mlp_io=None if traffic is None else round(traffic / io_bytes, 1))
+    kt = {k: {"launches": n, "avg_ms": round(m / n, 4), "roofline": mlp_roofline(k, n, m, u, dtype)}
           for k, (n, m, u) in ktimes.items()}
+    return value, elapsed / args.steps * 1e3, roofline, kt, train_stream, (cfg, net, ds)
 
-    render_s, grid, render_stream = None, None, None
-    if rank == 0 and not args.no_render and world == 1:
-        render_s, render_stream = render_frame_time(cfg, net, ds, device)
-        grid = grid_times(cfg, net, ds, device)
+
+def render_frame_time(cfg, net, ds, device, world, reps=2):
+    """800x800 hierarchical render of test view 0 (perturb 0), rays split over the ranks
+    (src/utils/dist_render.py) and gathered; max over ranks."""
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    from src.utils.dist_render import render_distributed
+    r = Renderer(net)
+    perturb = cfg.task_arg.perturb
+    cfg.task_arg.perturb = 0
+    rays, _ = ds.image_rays(0)
+    batch = {"rays": rays, "near": torch.tensor([2.0], device=device), "far": torch.tensor([6.0], device=device)}
+    net.eval()
+    times = []
+    keys = ("rgb_map_f", "depth_map_f", "acc_map_f")
+    with torch.no_grad():
+        render_distributed(r, batch, keys=keys)
+        for _ in range(reps):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            render_distributed(r, batch, keys=keys)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        stream = detail_times(lambda: r.render(batch)) if world == 1 else None
+    net.train()
+    cfg.task_arg.perturb = perturb
+    t = min(times)
+    if world > 1:
+        tt = torch.tensor([t], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt)
+    return t, stream
+
+
+def lego_grid():
+    import numpy as np
+    z = np.load(os.path.join(ROOT, "tests", "golden", "lego_occupancy_grid.npz"), allow_pickle=False)
+    shape = tuple(int(v) for v in z["shape"])
+    return torch.from_numpy(np.unpackbits(z["packed"])[: int(np.prod(shape))].reshape(shape).astype(bool))
+
+
+def grid_times(cfg, net, ds, device, reps=2):
+    """BASELINE config 4: the 128^3 x 8-corner occupancy bake (occupancy_grid.py:15-80) and the
+    grid-accelerated 800x800 march (render_accelerated, volume_renderer.py:268-357) of test
+    view 0 through the reference's own baked lego grid (tests/golden/lego_occupancy_grid.npz,
+    packed bits of logs/lego/occupancy_grid.pt).  Weights are the synthetic seed-0 init; the
+    bake is also timed with the coarse alpha bias shifted by +1 so that the threshold bites
+    (as the reference-generated res-8 bake golden does)."""
+    import contextlib
+    import io
+    from nerf_amd import ops
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    out = {}
+    with torch.no_grad():
+        for tag, shift in (("", 0.0), ("_shifted", 1.0)):
+            net.model.alpha_linear.bias += shift
+
+            def bake():
+                return ops.bake(net.model.packer(), 128, 1.0, dtype=cfg.task_arg.mlp_dtype)
+            bake()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                grid = bake()
+            torch.cuda.synchronize()
+            out[f"bake_s{tag}"] = round((time.perf_counter() - t0) / reps, 4)
+            out[f"bake_occupied{tag}"] = int(grid.sum())
+            net.model.alpha_linear.bias -= shift
+        r = Renderer(net)
+        r.set_occupancy_grid(lego_grid(), device)
+        rays, _ = ds.image_rays(0)
+        batch = {"rays": rays, "near": ops.device_scalar(2.0, device), "far": ops.device_scalar(6.0, device)}
+        with contextlib.redirect_stdout(io.StringIO()):
+            r.render_accelerated(batch)
+            times = []
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                o = r.render_accelerated(batch)
+                torch.cuda.synchronize()
+                times.append(time.perf_counter() - t0)
+        out["march_s_per_frame"] = round(min(times), 4)
+        out["march_queried_points"] = int(o["n_queried"])
+        if "n_evaluated" in o:
+            out["march_evaluated_points"] = int(o["n_evaluated"])
+    return out
+
+
+def _bench_rays(O, n, dev):
+    """Config-1 rays: pose_spherical(30,-30,4), uniform pixel ids of seed 0; gt rgb seed 1."""
+    pose = O.pose_spherical(30.0, -30.0, 4.0)
+    o, d = O.get_rays(800, 800, O.focal_from_angle(800, 0.6911112070083618), pose)
+    idx = torch.randint(0, 800 * 800, (n,), generator=torch.Generator().manual_seed(0))
+    rays = torch.cat([o.reshape(-1, 3)[idx], d.reshape(-1, 3)[idx]], 1)
+    gt = torch.rand(n, 3, generator=torch.Generator().manual_seed(1))
+    return rays.to(dev), gt.to(dev)
+
+
+def log(msg):
+    """Progress on stderr (the JSON line is the only stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def available_cpus():
+    """(cores this process may run on, how that was determined): the affinity mask, capped by
+    the cgroup CPU quota when one is set (a container's share of a larger host -- running
+    more threads than the quota only oversubscribes it)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    basis = "sched_getaffinity"
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    if quota is not None and quota < n:
+        n, basis = max(1, int(quota)), "cgroup cpu quota"
+    # the GPU box grants each GPU a share of its host's cores and states it in OMP_NUM_THREADS
+    # (os.cpu_count() there is the whole machine, shared with other jobs)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < n:
+        n, basis = int(omp), "OMP_NUM_THREADS (the CPU share granted to this GPU)"
+    return n, basis
+
+
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:  # noqa: BLE001 - reporting only
+        pass
+    return None
+
+
+def cpu_baseline(n_rays):
+    """Baseline leg: the oracle (tests-only CPU restatement of the reference op graph, torch
+    CPU) on a bounded sample -- config 1 of BASELINE.json, one n_rays forward+backward render
+    (perturb 0) -- on every host core available to this process."""
+    from oracle import nerf_oracle as O
+    threads, basis = available_cpus()
+    log(f"cpu baseline on {threads} threads ({basis})")
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        state = {k: v.clone().requires_grad_(True) for k, v in O.seeded_network_state(0).items()}
+        C, Fn = O.split_params(state, "model"), O.split_params(state, "model_fine")
+        rays, gt = _bench_rays(O, n_rays, "cpu")
+
+        def once():
+            for v in state.values():
+                v.grad = None
+            ret = O.render(C, Fn, rays, torch.tensor([2.0]), torch.tensor([6.0]))
+            O.loss_fn(ret, gt)[0].backward()
+
+        once()
+        t0 = time.perf_counter()
+        reps = 0
+        while reps < 5 and (reps < 2 or time.perf_counter() - t0 < 20.0):
+            once()
+            reps += 1
+        dt = (time.perf_counter() - t0) / reps
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": round(n_rays / dt, 2), "unit": "rays/s", "cores": threads, "cores_basis": basis,
+            "host_cpus": os.cpu_count(), "kind": "port", "cpu_model": cpu_model(), "torch": torch.__version__,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "sample": f"config 1: {n_rays}-ray forward+backward render (64+128 samples, perturb 0, seed-0 weights), "
+                      f"mean of {reps} after 1 warm-up, oracle restatement on torch CPU"}
+
+
+def eager_gpu_baseline(device, n_rays, dtype, reps=3):
+    """Baseline leg: the reference's per-step op graph (the oracle restatement of
+    volume_renderer.render + network.Network + MSE + clip_grad_value_(40) + Adam with one group
+    per tensor) run eagerly by PyTorch-ROCm on this GPU -- the "reference per-step PyTorch-ROCm
+    rays/s" of the north_star -- with the SAME MLP dtype (bf16 = torch.autocast) and perturb=1,
+    n_rays per step."""
+    from oracle import nerf_oracle as O
+    prm = {k: v.to(device).clone().requires_grad_(True) for k, v in O.seeded_network_state(0).items()}
+    C, Fn = O.split_params(prm, "model"), O.split_params(prm, "model_fine")
+    opt = torch.optim.Adam([{"params": [p]} for p in prm.values()], lr=5e-4, eps=1e-8)
+    rays, gt = _bench_rays(O, n_rays, device)
+    near, far = torch.tensor([2.0], device=device), torch.tensor([6.0], device=device)
+
+    def step():
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == "bf16"):
+            ret = O.render(C, Fn, rays, near, far, perturb=True)
+        O.loss_fn({k: v.float() for k, v in ret.items()}, gt)[0].backward()
+        torch.nn.utils.clip_grad_value_(list(prm.values()), 40.0)
+        opt.step()
+
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(n_rays / dt, 1), "unit": "rays/s", "kind": "pytorch_rocm_eager", "dtype": dtype,
+            "ms_per_step": round(dt * 1e3, 2),
+            "sample": f"{n_rays}-ray full train step (perturb 1, clip 40 + torch.optim.Adam), mean of {reps} "
+                      f"after 1 warm-up, reference op graph (oracle restatement) on PyTorch-ROCm {torch.__version__}"}
+
+
+def main():
+    args = parse()
+    world, rank, device = setup_dist()
+    second = {"fp32": "bf16", "bf16": "fp32"}[args.dtype]
+    lines = {}
+    for dtype in ([args.dtype] + ([] if args.no_second else [second])):
+        log(f"training {dtype}: {args.warmup} warmup + {args.steps} timed steps")
+        value, ms_step, roofline, kt, train_stream, (cfg, net, ds) = measure_training(args, world, rank, device, dtype)
+        render_s, render_stream, grid = None, None, None
+        log(f"{dtype}: {value:.0f} rays/s")
+        if not args.no_render:
+            render_s, render_stream = render_frame_time(cfg, net, ds, device, world)
+            log(f"{dtype}: render {render_s:.3f} s/frame")
+            if world == 1:
+                grid = grid_times(cfg, net, ds, device)
+                log(f"{dtype}: grid {grid}")
+        eager = None
+        if rank == 0 and world == 1 and not args.no_eager_baseline:
+            eager = eager_gpu_baseline(device, args.rays, dtype)
+            log(f"{dtype}: eager PyTorch-ROCm {eager['value']} rays/s")
+        lines[dtype] = {
+            "value": round(value, 1), "ms_per_step": round(ms_step, 3), "dtype": dtype,
+            "vs_baseline": None if eager is None else round(value / world / eager["value"], 2),
+            "baseline": eager, "roofline": roofline, "kernels": kt,
+            "stream_kernels": {"train_step": train_stream, "render_800x800": render_stream},
+            "render_s_per_frame": None if render_s is None else round(render_s, 4),
+            "render_parallelism": f"tile-split over {world} GPU(s)", "occupancy_grid": grid,
+        }
+        del net, ds
+        torch.cuda.empty_cache()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_rays)
+        log(f"cpu baseline {cpu['value']} rays/s")
 
     if rank == 0:
+        head = lines[args.dtype]
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "metric": METRIC, "value": head["value"], "unit": "rays/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": head["vs_baseline"], "dtype": args.dtype,
             "data": "synthetic (100 spherical 800x800 views, random rgb; seed-0 reference init)",
             "config": {"workload": "lego NeRF train step: coarse 64 + fine 128 samples/ray, 4096 rays/GPU, "
-                                   "MSE(c)+MSE(f), clip 40 + Adam",
+                                   "MSE(c)+MSE(f), clip 40 + Adam (BASELINE config 3)",
                        "rays_per_gpu": args.rays, "global_batch_rays": args.rays * world,
                        "samples_per_ray": 64 + 192, "parallelism": f"dp{world}"},
-            "roofline": roofline,
-            "kernels": kt,
-            "stream_kernels": {"train_step": train_stream, "render_800x800": render_stream},
-            "render_s_per_frame": None if render_s is None else round(render_s, 4),
-            "occupancy_grid": grid,
+            "roofline": head["roofline"],
             "cpu_baseline": cpu,
         }
+        line.update({k: v for k, v in head.items() if k not in line and k not in ("value", "dtype")})
+        line["baseline"] = head["baseline"]
+        if not args.no_second:
+            line[f"{second}_line"] = dict(lines[second], label=f"opt-in {second} MLP (same workload)",
+                                          metric=METRIC, unit="rays/s")
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -101,7 +101,7 @@ int64_t nerf_mlp_padded_samples(int64_t M);
 int64_t nerf_mlp_act_bytes(int dtype, int64_t M);
 int64_t nerf_mlp_dz_bytes(int dtype, int64_t M);
 int64_t nerf_mlp_mask_bytes(int64_t M);
-int64_t nerf_mlp_dw_items(int64_t M);  /* workgroups of the dW launch */
+int64_t nerf_mlp_dw_items(int dtype, int64_t M);  /* workgroups of the dW launch */
 int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void* packed_bwd, hipStream_t stream);
 int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const float* viewdirs, int samples_per_dir,
                  const int32_t* dir_index, int64_t M, int flags, float* raw, void* act, uint16_t* masks,

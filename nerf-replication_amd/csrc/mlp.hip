@@ -1086,10 +1086,23 @@ __device__ __forceinline__ bf16x8 dw_frag_bf16(const char* tile, int s, int lane
   short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, v);
 }
+// fp32 LDS swizzle of the dW ring.  The K = 2 fragment read below has the 32 lanes of one
+// ds_read_b32 bank group touch pieces p in {2 s + h, 2 s + h + 32} of all 4 chunks (dword
+// rho & 3 of each): as stored, those 8 pieces sit at the same (slot mod 8), i.e. on 4 of the
+// 32 banks -- an 8-way conflict.  Piece p of chunk c is placed at slot
+// (p & ~7) | ((p + 2 c + (p >> 5)) & 7) instead, which puts the 8 pieces on 8 distinct
+// (slot mod 8) and every read conflict-free.
+__host__ __device__ constexpr int dw_swz_f32(int c, int p) { return (p & ~7) | ((p + 2 * c + (p >> 5)) & 7); }
+__host__ __device__ constexpr int dw_unswz_f32(int c, int q) { return (q & ~7) | ((q - 2 * c - (q >> 5)) & 7); }
+
 // fp32: the K = 2 fragment (sample 2 s + h) of row (lane & 31)
+// (s = 4 a + b: slot dw_swz_f32(c, 2 s + h + 32 hp) = 8 a + 32 hp + ((2 b + h + 2 c + hp) & 7), so
+// the per-lane part depends on s & 3 only -- four hoisted bases + an immediate 128 a)
 __device__ __forceinline__ float dw_frag_f32(const char* tile, int s, int lane) {
-  const int rho = lane & 15, hp = (lane >> 4) & 1, h = lane >> 5;
-  return *(const float*)(tile + (rho >> 2) * 1024 + (2 * s + h + 32 * hp) * 16 + (rho & 3) * 4);
+  const int rho = lane & 15, hp = (lane >> 4) & 1, h = lane >> 5, c = rho >> 2;
+  const int b = s & 3, a = s >> 2;
+  const int lane_off = c * 1024 + 512 * hp + 16 * ((2 * b + h + 2 * c + hp) & 7) + 4 * (rho & 3);
+  return *(const float*)(tile + lane_off + 128 * a);
 }
 
 // one K step (16 samples bf16 / 2 samples fp32) of C += A B^T for A = LDS tile `at`
@@ -1165,7 +1178,7 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
     for (int q = 0; q < NT; ++q)
       if (q == slot) tau = q < JD.nd ? JD.dz[q] : JD.act[q - JD.nd];
     const int ntiles = is_dz ? ZT_TILES : AT_TILES;
-    const int piece = P::CH == 2 ? dw_unswz(c, lane) : lane;  // bf16 ring is swizzled (dw_swz)
+    const int piece = P::CH == 2 ? dw_unswz(c, lane) : dw_unswz_f32(c, lane);  // swizzled rings
     src[i] = (const char*)(is_dz ? a.dz : a.act) + tile_kib(a.nblk, ntiles, tau, 0, c, P::CH) * 1024 + piece * 16;
     bstride[i] = block_stride_kib(ntiles, P::CH) * 1024;
     dst[i] = (uint32_t)(slot * TB + c * 1024);
@@ -1389,20 +1402,43 @@ static int cu_count() {
     n = 256;
   return n;
 }
-static void dw_items(int64_t nblk, int item_off[NDWJOB + 1]) {
-  static const int target = cu_count();
-  int tiles = 0;
-  for (int j = 0; j < NDWJOB; ++j) tiles += dw_job_tiles(j);
-  item_off[0] = 0;
-  for (int j = 0; j < NDWJOB; ++j) {
-    int64_t n = target * (int64_t)dw_job_tiles(j) / tiles;
-    n = n < 1 ? 1 : n > nblk ? nblk : n;
-    item_off[j + 1] = item_off[j] + (int)n;
-  }
+// cost of one 32-sample block of job j: bf16 dW is HBM-bound (tile-blocks streamed), fp32 dW
+// is MFMA-bound (MFMAs of the job's busiest wave per K step: k-tiles, + the alpha row for
+// feature/alpha, 9 for the view layer's waves 0..3)
+static int dw_job_cost(int dtype, int j) {
+  if (dtype != 0) return dw_job_tiles(j);
+  return j < 8 ? gemm_k_tiles(j) : 9;
 }
-int64_t nerf_mlp_dw_items(int64_t M) {
+static void dw_items(int dtype, int64_t nblk, int item_off[NDWJOB + 1]) {
+  static const int target = cu_count();
+  int n[NDWJOB];
+  int64_t cost = 0;
+  for (int j = 0; j < NDWJOB; ++j) cost += dw_job_cost(dtype, j);
+  int total = 0;
+  for (int j = 0; j < NDWJOB; ++j) {
+    int64_t k = target * (int64_t)dw_job_cost(dtype, j) / cost;
+    n[j] = (int)(k < 1 ? 1 : k > nblk ? nblk : k);
+    total += n[j];
+  }
+  // the remaining CUs go, one at a time, to the job whose items are the longest
+  while (total < target) {
+    int best = -1;
+    double worst = 0.0;
+    for (int j = 0; j < NDWJOB; ++j) {
+      if (n[j] >= nblk) continue;
+      const double per = (double)dw_job_cost(dtype, j) / n[j];
+      if (per > worst) worst = per, best = j;
+    }
+    if (best < 0) break;
+    ++n[best];
+    ++total;
+  }
+  item_off[0] = 0;
+  for (int j = 0; j < NDWJOB; ++j) item_off[j + 1] = item_off[j] + n[j];
+}
+int64_t nerf_mlp_dw_items(int dtype, int64_t M) {
   int off[NDWJOB + 1];
-  dw_items(nerf_mlp_padded_samples(M) / 32, off);
+  dw_items(dtype, nerf_mlp_padded_samples(M) / 32, off);
   return off[NDWJOB];
 }
 
@@ -1428,7 +1464,7 @@ int nerf_mlp_bwd_dw(int dtype, int64_t M, const void* act, const void* dz, float
   NERF_REQUIRE(act && dz && grad, "nerf_mlp_bwd_dw: null pointer");
   const int64_t nblk = nerf_mlp_padded_samples(M) / 32;
   DwArgs w{dz, act, nblk, grad, {}};
-  dw_items(nblk, w.item_off);
+  dw_items(dtype, nblk, w.item_off);
   dim3 grid((unsigned)w.item_off[NDWJOB]);
   if (dtype == 0) {
     allow_lds(dw_kernel<PF32>, dw_lds_bytes<PF32>());

@@ -39,7 +39,7 @@ SIGNATURES = {
     "nerf_mlp_act_bytes": (_i64, [_i32, _i64]),
     "nerf_mlp_dz_bytes": (_i64, [_i32, _i64]),
     "nerf_mlp_mask_bytes": (_i64, [_i64]),
-    "nerf_mlp_dw_items": (_i64, [_i64]),
+    "nerf_mlp_dw_items": (_i64, [_i32, _i64]),
     "nerf_mlp_pack": (_i32, [_p, _i32, _p, _p, _p]),
     "nerf_mlp_fwd": (_i32, [_p, _i32, _p, _p, _i32, _p, _i64, _i32, _p, _p, _p, _p]),
     "nerf_mlp_bwd": (_i32, [_p, _i32, _p, _i64, _p, _p, _p, _p, _p]),

@@ -309,6 +309,23 @@ NET_PARAM_NAMES = (
 
 
 _PARAM_GENERATION = [0]
+_DIRECT_GRAD = [0]
+
+
+class direct_grad:
+    """Context for a plain ``loss.backward()`` of a training step whose parameters' ``.grad``
+    are views of one flat buffer (FusedAdam): inside it the dW kernel adds straight into
+    ``.grad`` (no zero-filled temporary, no 24 autograd accumulations) and autograd receives
+    None for the parameters.  Outside it (``torch.autograd.grad``, hooks, a non-flat
+    optimizer) the MLP backward returns ordinary gradients to autograd."""
+
+    def __enter__(self):
+        _DIRECT_GRAD[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _DIRECT_GRAD[0] -= 1
+        return False
 
 
 def params_updated() -> None:
@@ -329,6 +346,22 @@ class PackedMLP:
         # called as grad_ready(flat_grad_view) once this net's gradient is complete in a
         # backward pass (the data-parallel trainer starts its all-reduce bucket there)
         self.grad_ready = None
+        # training forwards of this net whose backward has not run yet: a render split into
+        # chunks (volume_renderer.py:62-67) calls the MLP once per chunk, and the net's
+        # gradient is complete only after the LAST of those backwards
+        self.pending = 0
+
+    def forward_started(self) -> None:
+        self.pending += 1
+
+    def backward_done(self, flat: Optional[torch.Tensor]) -> bool:
+        """One training forward's backward has been enqueued; fires grad_ready(flat) when it
+        was the last pending one.  Returns True when it fired."""
+        self.pending = max(0, self.pending - 1)
+        if self.pending == 0 and self.grad_ready is not None:
+            self.grad_ready(flat)
+            return True
+        return False
 
     def flat_grad(self) -> Optional[torch.Tensor]:
         """The 24 .grad tensors as one flat fp32 view, when they are laid out back to back in
@@ -403,6 +436,7 @@ class _MLP(torch.autograd.Function):
         ctx.act, ctx.masks = act, masks
         if store:
             ctx.packed_bwd = packer.get(dtype, 1)
+            packer.forward_started()
         return raw
 
     @staticmethod
@@ -414,9 +448,10 @@ class _MLP(torch.autograd.Function):
         dev = g_raw.device
         g_raw = g_raw.contiguous()
         dz = torch.empty(lib().nerf_mlp_dz_bytes(ctx.dtype, ctx.M), dtype=torch.uint8, device=dev)
-        # accumulate straight into the parameters' .grad when they are one flat buffer (the
-        # dW kernel adds with atomics): no zero-fill, no 24 autograd accumulation kernels
-        direct = ctx.packer.flat_grad()
+        # inside ops.direct_grad() (a training step's loss.backward()), accumulate straight into
+        # the parameters' .grad when they are one flat buffer (the dW kernel adds with atomics):
+        # no zero-fill, no 24 autograd accumulation kernels
+        direct = ctx.packer.flat_grad() if _DIRECT_GRAD[0] > 0 else None
         grad = direct if direct is not None else torch.zeros(lib().nerf_mlp_net_params(), device=dev,
                                                               dtype=torch.float32)
         s = stream_of(g_raw)
@@ -426,8 +461,8 @@ class _MLP(torch.autograd.Function):
         with kernel_timer("mlp_bwd_dw", ctx.M):
             check(lib().nerf_mlp_bwd_dw(ctx.dtype, ctx.M, ptr(ctx.act), ptr(dz), ptr(grad), s), "nerf_mlp_bwd_dw")
         ctx.act = ctx.masks = None
-        if ctx.packer.grad_ready is not None:
-            ctx.packer.grad_ready(grad if direct is not None else None)
+        # the net's data-parallel bucket starts after its last pending chunk's dW only
+        ctx.packer.backward_done(grad if direct is not None else None)
         if direct is not None:
             return nones + (None,) * len(params)
         out, off = [], 0

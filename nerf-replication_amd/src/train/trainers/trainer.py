@@ -49,10 +49,18 @@ class GradBuckets:
     def __init__(self):
         self.works = []
         self.done = []
+        self.packers = []
 
     def attach(self, packers):
-        for pk in packers:
+        self.packers = list(packers)
+        for pk in self.packers:
             pk.grad_ready = self._hook
+
+    def begin(self) -> None:
+        """Start of a step: forget forwards whose backward never ran (an aborted step), so a
+        net's bucket fires after exactly this step's last chunk."""
+        for pk in self.packers:
+            pk.pending = 0
 
     def _hook(self, flat):
         if flat is None or dist_world() == 1:
@@ -88,8 +96,9 @@ class Trainer:
         self.global_step = 0
         self.clip_value = 40.0
         self.buckets = GradBuckets()
+        self.buckets.packers = [m.packer() for m in self.network.modules() if hasattr(m, "packer")]
         if dist_world() > 1:
-            self.buckets.attach([m.packer() for m in self.network.modules() if hasattr(m, "packer")])
+            self.buckets.attach(self.buckets.packers)
 
     def reduce_loss_stats(self, loss_stats):
         return {k: torch.mean(v) for k, v in loss_stats.items()}
@@ -107,10 +116,14 @@ class Trainer:
 
     def train_step(self, batch, optimizer):
         """render -> loss -> backward -> all-reduce -> fused clip + Adam. Returns (loss, stats)."""
+        from nerf_amd import ops
+        self.buckets.begin()
         output, loss, loss_stats = self.network(batch)
         loss = loss.mean()
         optimizer.zero_grad()
-        loss.backward()  # per-net all-reduce buckets start inside (GradBuckets)
+        # dW straight into FusedAdam's flat .grad; per-net all-reduce buckets start inside
+        with ops.direct_grad():
+            loss.backward()
         self.buckets.finish(optimizer)
         optimizer.clip_value = self.clip_value
         optimizer.step()

@@ -60,13 +60,53 @@ def _worker(rank, world, port, q):
     bk._hook(opt.flat_grad[2:6])
     bk.finish(opt)
     bucket_grad = opt.flat_grad.tolist()
+    # a two-chunk training step (train_rays = 2 x chunk_size): each net's MLP runs once per
+    # chunk, its bucket must fire once, after the LAST chunk's backward (ops.PackedMLP
+    # pending count), and the bucketed average must equal the plain flat average
+    from nerf_amd.ops import PackedMLP
+    coarse = PackedMLP([torch.zeros(1)] * 24)
+    fine = PackedMLP([torch.zeros(1)] * 24)
+    flat = torch.zeros(10)
+    opt.flat_grad = flat
+    bk = GradBuckets()
+    bk.attach([coarse, fine])
+    bk.begin()
+    g = torch.Generator().manual_seed(100 + rank)
+    parts = {k: torch.randn(n, generator=g) for k, n in (("c1", 6), ("c2", 6), ("f1", 4), ("f2", 4))}
+    for _ in range(2):  # forward: chunk 1 then chunk 2, coarse then fine
+        coarse.forward_started()
+        fine.forward_started()
+    fired = []
+    # backward in reverse: chunk 2 (fine, coarse), then chunk 1 (fine, coarse)
+    for key, pk, sl in (("f2", fine, slice(6, 10)), ("c2", coarse, slice(0, 6)), ("f1", fine, slice(6, 10)),
+                        ("c1", coarse, slice(0, 6))):
+        flat[sl] += parts[key]
+        fired.append(pk.backward_done(flat[sl]))
+    n_works = len(bk.works)
+    bk.finish(opt)
+    local = torch.cat([parts["c1"] + parts["c2"], parts["f1"] + parts["f2"]])
+    plain = local.clone()
+    dist.all_reduce(plain)
+    plain /= world
+    two_chunk_ok = fired == [False, False, True, True] and n_works == 2 and torch.allclose(flat, plain, atol=1e-6)
+    # rank-distinct ray streams (the reference's fix_random makes every rank draw the same
+    # rays, blender.py:126 + train.py:25-28; here the Philox seeds differ per rank)
+    from src.datasets.nerf.blender import Dataset
+    torch.manual_seed(0)  # identical torch seed on every rank, as fix_random would set
+    ds = Dataset.from_arrays(torch.zeros(1, 2, 2, 3), torch.eye(4)[None], 1.0)
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    seeds = torch.tensor([ds.seed & 0xFFFFFFFF, Renderer(None)._seed & 0xFFFFFFFF], dtype=torch.int64)
+    all_seeds = [torch.zeros_like(seeds) for _ in range(world)]
+    dist.all_gather(all_seeds, seeds)
+    seeds_distinct = len({tuple(s.tolist()) for s in all_seeds}) == world
     # tile-split inference: 1001 rays over the ranks, gathered everywhere
     from src.utils.dist_render import render_distributed
     rays = torch.arange(1001 * 6, dtype=torch.float32).reshape(1, 1001, 6)
     full = _FakeRenderer().render({"rays": rays})
     got = render_distributed(_FakeRenderer(), {"rays": rays})
     ok = all(torch.equal(got[k], full[k]) for k in ("rgb_map_f", "depth_map_f", "acc_map_f"))
-    q.put((rank, opt_grad_plain, float(lin.weight.sum()), bucket_grad, ok and got["n_queried"] == 1001))
+    q.put((rank, opt_grad_plain, float(lin.weight.sum()), bucket_grad, ok and got["n_queried"] == 1001,
+           two_chunk_ok, seeds_distinct))
     dist.destroy_process_group()
 
 
@@ -82,8 +122,10 @@ def test_two_rank_gradient_average_and_broadcast():
         p.join(timeout=60)
         assert p.exitcode == 0
     expect = [1.5 * i for i in range(10)]
-    for rank, grad, wsum, bucket_grad, render_ok in res:
+    for rank, grad, wsum, bucket_grad, render_ok, two_chunk_ok, seeds_distinct in res:
         assert grad == pytest.approx(expect)
         assert wsum == 0.0  # rank 0's weights everywhere
         assert bucket_grad == pytest.approx(expect)  # bucketed + remainder == one flat average
         assert render_ok  # tile-split render == single-process render
+        assert two_chunk_ok  # one bucket per net after its last chunk; == the flat average
+        assert seeds_distinct  # every rank draws its own rays
