@@ -139,7 +139,10 @@ int nerf_bake_reduce(const float* raw, int res, int dedup, float threshold, uint
 
 /* ---- (a12) grid-accelerated march (render_accelerated, volume_renderer.py:268-357) --------------
  * Round structure: init; repeat { zero counters; gather (<= K occupied steps per alive ray,
- * compacted points); fine MLP on the points; composite (stops at T < t_thresh) } until no
+ * compacted points; cap = room for points, K <= cap <= INT32_MAX -- size it alive rays x K, a ray
+ * that finds no room keeps its position for the next round); fine MLP on the points; composite
+ * (stops at T < t_thresh; consumed (nullable, uint64) += the points composited, i.e. the
+ * reference's MLP queries -- points gathered past a ray's termination are dropped) } until no
  * ray is alive; finish (white background). */
 int nerf_march_init(float* T, float* rgb, float* depth, float* acc, int32_t* next_step, uint8_t* alive,
                     uint8_t* exhausted, int64_t N, hipStream_t stream);
@@ -151,7 +154,7 @@ int nerf_march_gather(const float* rays, int64_t N, const float* t_table, int n_
 int nerf_march_composite(const float* raw, const float* rays, int64_t N, const float* t_table, const int32_t* ray_off,
                          const int32_t* ray_cnt, const int32_t* out_step, float* T, float* rgb, float* depth,
                          float* acc, int32_t* next_step, uint8_t* alive, uint8_t* exhausted, float step_size,
-                         float t_thresh, hipStream_t stream);
+                         float t_thresh, unsigned long long* consumed, hipStream_t stream);
 int nerf_march_finish(float* rgb, const float* acc, int64_t N, int white, hipStream_t stream);
 
 /* ---- (a10) clip_grad_value_ + Adam (src/train/trainers/trainer.py:61-62, optimizer.py:8-28) ---- */

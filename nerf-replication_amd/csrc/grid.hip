@@ -191,8 +191,10 @@ __global__ void march_gather_kernel(MarchGatherArgs a) {
   const bool overflow = (int64_t)pos + cnt > a.cap;
   a.ray_off[r] = pos;
   a.ray_cnt[r] = overflow ? 0 : cnt;
+  // out of room (the caller sizes cap = alive rays x K, so never taken): the ray keeps its
+  // position and gathers again next round
+  if (overflow) return;
   a.st.exhausted[r] = (s >= a.n_steps) ? 1 : 0;
-  if (overflow) return;  // caller sizes cap = N*K, never taken
   a.st.next_step[r] = s;
 }
 
@@ -235,11 +237,33 @@ struct MarchCompArgs {
   const int32_t* out_step;
   MarchState st;
   float step_size, t_thresh;
+  unsigned long long* consumed;  // += points composited (the reference's MLP queries) or null
 };
 
+__device__ __forceinline__ int march_composite_ray_impl(const MarchCompArgs& a, int64_t r);
+__device__ __forceinline__ int march_composite_ray(const MarchCompArgs& a, int64_t r) {
+  return march_composite_ray_impl(a, r);
+}
+
+// Composites a ray's gathered points in step order and stops at T < t_thresh
+// (volume_renderer.py:327-341).  Points gathered past that step were evaluated speculatively
+// and are dropped; the points composited are exactly the reference's queries (:324), counted
+// into `consumed`.
 __global__ void march_composite_kernel(MarchCompArgs a) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= a.N || !a.st.alive[r]) return;
+  const bool live = r < a.N && a.st.alive[r];
+  int used = 0;
+  if (live) used = march_composite_ray(a, r);
+  if (a.consumed) {
+    // wave-aggregated count
+    int tot = used;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    if (lane_id() == 0 && tot) atomicAdd(a.consumed, (unsigned long long)tot);
+  }
+}
+
+__device__ __forceinline__ int march_composite_ray_impl(const MarchCompArgs& a, int64_t r) {
   const int cnt = a.ray_cnt[r], off = a.ray_off[r];
   const float* ray = a.rays + r * 6;
   const float dx = ray[3], dy = ray[4], dz = ray[5];
@@ -248,6 +272,7 @@ __global__ void march_composite_kernel(MarchCompArgs a) {
   float cr = a.st.rgb[r * 3 + 0], cg = a.st.rgb[r * 3 + 1], cb = a.st.rgb[r * 3 + 2];
   float dep = a.st.depth[r], acc = a.st.acc[r];
   bool alive = true;
+  int used = cnt;
   for (int k = 0; k < cnt; ++k) {
     const float4 rw = *(const float4*)(a.raw + (int64_t)(off + k) * 4);
     const float t = a.t_table[a.out_step[off + k]];
@@ -263,6 +288,7 @@ __global__ void march_composite_kernel(MarchCompArgs a) {
     T = fmul(T, fsub(1.f, alpha));
     if (T < a.t_thresh) {
       alive = false;
+      used = k + 1;
       break;
     }
   }
@@ -273,6 +299,7 @@ __global__ void march_composite_kernel(MarchCompArgs a) {
   a.st.depth[r] = dep;
   a.st.acc[r] = acc;
   if (!alive || a.st.exhausted[r]) a.st.alive[r] = 0;
+  return used;
 }
 
 struct MarchInitArgs { MarchState st; int64_t N; };
@@ -365,7 +392,7 @@ int nerf_march_gather(const float* rays, int64_t N, const float* t_table, int n_
                       int32_t* start_step_scratch, int32_t* out_ray, int32_t* out_step, float* out_pts,
                       int32_t* ray_off, int32_t* ray_cnt, int64_t cap, hipStream_t stream) {
   NERF_REQUIRE(N >= 0 && n_steps >= 0 && K > 0 && res > 1 && bbox_host, "nerf_march_gather: bad arguments");
-  NERF_REQUIRE(cap >= N * (int64_t)K, "nerf_march_gather: cap must be >= N*K");
+  NERF_REQUIRE(cap >= K && cap <= INT32_MAX, "nerf_march_gather: need K <= cap <= INT32_MAX (point offsets are int32)");
   if (N == 0) return 0;
   MarchGatherArgs a{rays, N, t_table, n_steps, grid, res, make_bbox(bbox_host), K,
                     {T, rgb, depth, acc, next_step, alive, exhausted},
@@ -385,10 +412,10 @@ int nerf_march_gather(const float* rays, int64_t N, const float* t_table, int n_
 int nerf_march_composite(const float* raw, const float* rays, int64_t N, const float* t_table, const int32_t* ray_off,
                          const int32_t* ray_cnt, const int32_t* out_step, float* T, float* rgb, float* depth,
                          float* acc, int32_t* next_step, uint8_t* alive, uint8_t* exhausted, float step_size,
-                         float t_thresh, hipStream_t stream) {
+                         float t_thresh, unsigned long long* consumed, hipStream_t stream) {
   if (N == 0) return 0;
   MarchCompArgs a{raw, rays, N, t_table, ray_off, ray_cnt, out_step,
-                  {T, rgb, depth, acc, next_step, alive, exhausted}, step_size, t_thresh};
+                  {T, rgb, depth, acc, next_step, alive, exhausted}, step_size, t_thresh, consumed};
   hipLaunchKernelGGL(march_composite_kernel, grid1(N), dim3(256), 0, stream, a);
   return check_launch("nerf_march_composite");
 }

@@ -1095,14 +1095,36 @@ __device__ __forceinline__ bf16x8 dw_frag_bf16(const char* tile, int s, int lane
 __host__ __device__ constexpr int dw_swz_f32(int c, int p) { return (p & ~7) | ((p + 2 * c + (p >> 5)) & 7); }
 __host__ __device__ constexpr int dw_unswz_f32(int c, int q) { return (q & ~7) | ((q - 2 * c - (q >> 5)) & 7); }
 
-// fp32: the K = 2 fragment (sample 2 s + h) of row (lane & 31)
-// (s = 4 a + b: slot dw_swz_f32(c, 2 s + h + 32 hp) = 8 a + 32 hp + ((2 b + h + 2 c + hp) & 7), so
-// the per-lane part depends on s & 3 only -- four hoisted bases + an immediate 128 a)
-__device__ __forceinline__ float dw_frag_f32(const char* tile, int s, int lane) {
+// fp32: the K = 2 fragment (sample 2 s + h) of row (lane & 31).  With s = 4 a + b, the slot
+// dw_swz_f32(c, 2 s + h + 32 hp) = 8 a + 32 hp + ((2 b + h + 2 c + hp) & 7): the per-lane part
+// depends on s & 3 only.  A tile region's four per-lane bases (F32Base) are laundered through
+// empty asm, so every read is one ds_read_b32 at base + immediate (tile * 4 KiB + 128 a).
+#ifndef NERF_DW_SWZ_F32
+#define NERF_DW_SWZ_F32 1
+#endif
+__device__ __forceinline__ uint32_t dw_f32_lane_off(int lane, int b) {
   const int rho = lane & 15, hp = (lane >> 4) & 1, h = lane >> 5, c = rho >> 2;
-  const int b = s & 3, a = s >> 2;
-  const int lane_off = c * 1024 + 512 * hp + 16 * ((2 * b + h + 2 * c + hp) & 7) + 4 * (rho & 3);
-  return *(const float*)(tile + lane_off + 128 * a);
+  const int sw = NERF_DW_SWZ_F32 ? 2 * c + hp : 0;
+  return (uint32_t)(c * 1024 + 512 * hp + 16 * ((2 * b + h + sw) & 7) + 4 * (rho & 3));
+}
+struct F32Base { uint32_t b[4]; };
+__device__ __forceinline__ F32Base f32_base(uint32_t region, const uint32_t (&lane_off)[4]) {
+  F32Base r;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    r.b[b] = region + lane_off[b];
+    settle(r.b[b]);
+  }
+  return r;
+}
+typedef __attribute__((address_space(3))) const float lds_cf;
+template <int IMM>
+__device__ __forceinline__ float f32_frag(const F32Base& B, int s) {
+  static_assert(IMM >= 0 && IMM + 128 * 3 < 65536, "ds_read offset is 16 bits");
+  return *(lds_cf*)(uintptr_t)(B.b[s & 3] + (uint32_t)(IMM + 128 * (s >> 2)));
+}
+__device__ __forceinline__ float dw_frag_f32(const char* tile, int s, int lane) {
+  return *(const float*)(tile + dw_f32_lane_off(lane, s & 3) + 128 * (s >> 2));
 }
 
 // one K step (16 samples bf16 / 2 samples fp32) of C += A B^T for A = LDS tile `at`
@@ -1151,6 +1173,25 @@ __device__ __forceinline__ void dw_flush_bias(float* grad, int ntile, int nvalid
   if (lane < 32 && n < nvalid) atomicAdd(grad + OFF + n, dbias);
 }
 
+// LDS slot of job tile q (q < nd: dz tile q, else act tile q - nd): the act tiles come first,
+// so a K step's act-tile reads are one per-lane base + immediates below 64 KiB
+__host__ __device__ constexpr int dw_slot(const DwJobDesc& d, int q) { return q < d.nd ? d.na + q : q - d.nd; }
+
+// global_load_lds_dwordx4 with a uniform 64-bit base (SGPR pair) + per-lane 32-bit offset
+// (the SADDR form: one VGPR per fetch stream instead of a 64-bit address pair)
+__device__ __forceinline__ void glds16_saddr(const void* sbase, uint32_t voff, uint32_t lds_wave_base) {
+  uint32_t saved;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(saved) : "v"(voff), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds_wave_base)) : "memory");
+}
+
+// a wave-uniform pointer made visibly uniform (SGPR pair) to the compiler
+__device__ __forceinline__ const char* uniform_ptr(const char* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const char*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
 template <class P, int J>
 __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t b_end, char* lds) {
   constexpr DwJobDesc JD = dw_job_desc(J);
@@ -1161,39 +1202,48 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
   constexpr int G = (NCHUNK + DW_WAVES - 1) / DW_WAVES;  // DMA per wave per block (uniform)
   constexpr int NBUF = dw_nbuf<P>(), D = NBUF - 1;
   constexpr int KS = P::CH == 2 ? 2 : 16;    // K steps per 32-sample block
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;  // (kept divergent to the compiler: uniform branching spills)
 
-  // DMA sources / LDS offsets, resolved once (a table lookup inside the loop would be a
-  // compiler-visible load, whose wait drains the ring)
-  const char* src[G];
+  // DMA streams, resolved once (a table lookup inside the loop would be a compiler-visible
+  // load, whose wait drains the ring): uniform tile base (block 0) + per-lane piece offset
+  const char* sb[G];
+  uint32_t voff[G];
   uint32_t dst[G];
   int64_t bstride[G];
 #pragma unroll
   for (int i = 0; i < G; ++i) {
     const int k = cmin(wave + DW_WAVES * i, NCHUNK - 1);
-    const int slot = k / P::CH, c = k % P::CH;
-    const bool is_dz = slot < JD.nd;
+    const int q = k / P::CH, c = k % P::CH;
+    const bool is_dz = q < JD.nd;
     int tau = 0;
 #pragma unroll
-    for (int q = 0; q < NT; ++q)
-      if (q == slot) tau = q < JD.nd ? JD.dz[q] : JD.act[q - JD.nd];
+    for (int t = 0; t < NT; ++t)
+      if (t == q) tau = t < JD.nd ? JD.dz[t] : JD.act[t - JD.nd];
     const int ntiles = is_dz ? ZT_TILES : AT_TILES;
-    const int piece = P::CH == 2 ? dw_unswz(c, lane) : dw_unswz_f32(c, lane);  // swizzled rings
-    src[i] = (const char*)(is_dz ? a.dz : a.act) + tile_kib(a.nblk, ntiles, tau, 0, c, P::CH) * 1024 + piece * 16;
+    const int piece = P::CH == 2 ? dw_unswz(c, lane) : NERF_DW_SWZ_F32 ? dw_unswz_f32(c, lane) : lane;  // swizzled
+    sb[i] = uniform_ptr((const char*)(is_dz ? a.dz : a.act) + tile_kib(a.nblk, ntiles, tau, 0, c, P::CH) * 1024);
+    voff[i] = (uint32_t)(piece * 16);
     bstride[i] = block_stride_kib(ntiles, P::CH) * 1024;
+    int slot = 0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      if (t == q) slot = dw_slot(JD, t);
     dst[i] = (uint32_t)(slot * TB + c * 1024);
   }
   const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_void*)lds;
   auto fetch = [&](int64_t b, int buf) {
 #pragma unroll
-    for (int i = 0; i < G; ++i) glds16_asm(src[i] + b * bstride[i], lds_base + (uint32_t)(buf * BUF) + dst[i]);
+    for (int i = 0; i < G; ++i)
+      glds16_saddr(uniform_ptr(sb[i] + b * bstride[i]), voff[i], lds_base + (uint32_t)(buf * BUF) + dst[i]);
   };
 
   // wave roles
-  //   REG: n slot w, k slots nd .. nd + kt;  FA: + alpha (slot 8) x k slot nd + w
-  //   VR: waves 0..3 n slot w, k slots nd .. nd + 9; waves 4..7 n slot 4 (d rgb) x slot nd + 9 + (w - 4)
+  //   REG: dz tile w x act tiles 0 .. kt;  FA: + alpha (dz tile 8) x act tile w
+  //   VR: waves 0..3 dz tile w x act tiles 0 .. 9; waves 4..7 d rgb (dz tile 4) x act tile 9 + (w - 4)
   const bool vr_rgb = JD.kind == DW_VR && wave >= 4;
-  const int n_slot = vr_rgb ? 4 : wave;
+  const int n_q = vr_rgb ? 4 : wave;         // dz tile of this wave
+  const int n_lds = JD.na + n_q;             // its LDS slot
   f32x16 acc[10], acc2;
 #pragma unroll
   for (int t = 0; t < 10; ++t)
@@ -1202,6 +1252,9 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc2[i] = 0.f;
   float dbias = 0.f, dbias2 = 0.f;
+  uint32_t lane_off[4];
+#pragma unroll
+  for (int bb = 0; bb < 4; ++bb) lane_off[bb] = dw_f32_lane_off(lane, bb);
 
   for (int d = 0; d < D; ++d)
     if (b_begin + d < b_end) fetch(b_begin + d, d);
@@ -1213,21 +1266,62 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
     __builtin_amdgcn_sched_barrier(0);
     if (b + D < b_end) fetch(b + D, buf == 0 ? NBUF - 1 : buf - 1);
     const char* tiles = lds + buf * BUF;
-    const char* nt = tiles + n_slot * TB;
+    if constexpr (P::CH == 4) {
+      // 16 K steps as 4 rounds of 4 (s = 4 a + b): the rounds are a real loop (the bases step
+      // by 128 B), so the scheduler's window -- and the fragments it keeps in flight -- is
+      // one round, not the whole block
+      const uint32_t region = lds_base + (uint32_t)(buf * BUF);
+      uint32_t rn = region + (uint32_t)(n_lds * TB);
+      // act tiles: all of them from slot 0 (immediates t * 4 KiB), or the rgb wave's one
+      uint32_t ra = region + (uint32_t)(vr_rgb ? (9 + wave - 4) * TB : 0);
+      uint32_t ral = region + (uint32_t)((JD.na + 8) * TB), rw = region + (uint32_t)(wave * TB);
+#pragma nounroll
+      for (int ar = 0; ar < 4; ++ar) {
+        const F32Base Bn = f32_base(rn, lane_off), Ba = f32_base(ra, lane_off);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      if (!vr_rgb) {
-        dbias += dw_rowsum<P>(nt, s, lane);
+        for (int s = 0; s < 4; ++s) {
+          const float an = f32_frag<0>(Bn, s);
+          dbias += an;
+          if (!vr_rgb) {
+            sfor<JD.kt>([&](auto tt) {
+              constexpr int t = decltype(tt)::value;
+              acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(an, f32_frag<t * TB>(Ba, s), acc[t], 0, 0, 0);
+            });
+          } else {
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(an, f32_frag<0>(Ba, s), acc[0], 0, 0, 0);
+          }
+        }
+        if constexpr (JD.kind == DW_FA) {
+          const F32Base Bal = f32_base(ral, lane_off), Bw = f32_base(rw, lane_off);
 #pragma unroll
-        for (int t = 0; t < JD.kt; ++t) acc[t] = dw_mma<P>(nt, tiles + (JD.nd + t) * TB, s, lane, acc[t]);
-      } else {
-        dbias += dw_rowsum<P>(nt, s, lane);
-        acc[0] = dw_mma<P>(nt, tiles + (JD.nd + 9 + (wave - 4)) * TB, s, lane, acc[0]);
+          for (int s = 0; s < 4; ++s) {
+            const float al = f32_frag<0>(Bal, s);
+            if (wave == 0) dbias2 += al;
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(al, f32_frag<0>(Bw, s), acc2, 0, 0, 0);
+          }
+        }
+        rn += 128;
+        ra += 128;
+        ral += 128;
+        rw += 128;
       }
-      if constexpr (JD.kind == DW_FA) {
-        const char* at = tiles + 8 * TB;
-        if (wave == 0) dbias2 += dw_rowsum<P>(at, s, lane);
-        acc2 = dw_mma<P>(at, tiles + (JD.nd + wave) * TB, s, lane, acc2);
+    } else {
+      const char* nt = tiles + n_lds * TB;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        if (!vr_rgb) {
+          dbias += dw_rowsum<P>(nt, s, lane);
+#pragma unroll
+          for (int t = 0; t < JD.kt; ++t) acc[t] = dw_mma<P>(nt, tiles + t * TB, s, lane, acc[t]);
+        } else {
+          dbias += dw_rowsum<P>(nt, s, lane);
+          acc[0] = dw_mma<P>(nt, tiles + (9 + (wave - 4)) * TB, s, lane, acc[0]);
+        }
+        if constexpr (JD.kind == DW_FA) {
+          const char* at = tiles + (JD.na + 8) * TB;
+          if (wave == 0) dbias2 += dw_rowsum<P>(at, s, lane);
+          acc2 = dw_mma<P>(at, tiles + wave * TB, s, lane, acc2);
+        }
       }
     }
     buf = buf == NBUF - 1 ? 0 : buf + 1;
@@ -1405,8 +1499,11 @@ static int cu_count() {
 // cost of one 32-sample block of job j: bf16 dW is HBM-bound (tile-blocks streamed), fp32 dW
 // is MFMA-bound (MFMAs of the job's busiest wave per K step: k-tiles, + the alpha row for
 // feature/alpha, 9 for the view layer's waves 0..3)
+#ifndef NERF_DW_BALANCE_MFMA
+#define NERF_DW_BALANCE_MFMA 0  /* measured: byte-balanced items are 2 % faster in fp32 too */
+#endif
 static int dw_job_cost(int dtype, int j) {
-  if (dtype != 0) return dw_job_tiles(j);
+  if (dtype != 0 || !NERF_DW_BALANCE_MFMA) return dw_job_tiles(j);
   return j < 8 ? gemm_k_tiles(j) : 9;
 }
 static void dw_items(int dtype, int64_t nblk, int item_off[NDWJOB + 1]) {

@@ -541,11 +541,22 @@ def bake(packer: PackedMLP, res: int, threshold: float, bbox=SCENE_BBOX, dtype=F
     return grid.bool()
 
 
+MARCH_POINT_BYTES = 4 + 4 + 12 + 16  # out_ray, out_step, out_pts, raw per gathered point
+
+
 def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: torch.Tensor, step_size: float = 0.005,
           t_thresh: float = 1e-4, bbox=SCENE_BBOX, white_bkgd: bool = True, dtype=F32,
-          t_table: Optional[torch.Tensor] = None, k_schedule=(16, 32, 64, 128, 256, 512, 1024)):
+          t_table: Optional[torch.Tensor] = None, k_schedule=(16, 32, 64, 128, 256, 512, 1024),
+          round_bytes: int = 1 << 31):
     """Grid-accelerated march with early termination -> dict(rgb_map_f, depth_map_f,
-    acc_map_f, n_queried, rounds)."""
+    acc_map_f, n_queried, n_evaluated, rounds).
+
+    Each round gathers up to K occupied steps of every alive ray and evaluates them in one MLP
+    launch; compositing stops at T < t_thresh, so points past a ray's termination were
+    evaluated speculatively.  n_queried counts the composited points only -- exactly the
+    reference's MLP queries (volume_renderer.py:324) -- and n_evaluated every point the MLP ran
+    on.  A round's point buffers are sized alive rays x K, with K capped so they stay within
+    round_bytes (and int32 offsets)."""
     rays = _f32c(rays.reshape(-1, 6), "rays")
     dev, N = rays.device, rays.shape[0]
     L = lib()
@@ -567,15 +578,17 @@ def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: 
     off = torch.empty(N, dtype=torch.int32, device=dev)
     cnt = torch.empty(N, dtype=torch.int32, device=dev)
     counters = torch.zeros(2, dtype=torch.int32, device=dev)
+    consumed = torch.zeros(1, dtype=torch.int64, device=dev)
     # unit view directions of every ray (d / |d|), as render_accelerated computes per query
     _, _, vd = sample_stratified(rays, near, far, 1, False, want_pts=False)
     check(L.nerf_march_init(ptr(T), ptr(rgb), ptr(depth), ptr(acc), ptr(nxt), ptr(alive), ptr(exh), N, s),
           "nerf_march_init")
     bb = _bbox_arr(bbox)
-    queried, rounds, ki = 0, 0, 0
+    evaluated, rounds, ki, n_alive = 0, 0, 0, N
     while True:
         K = k_schedule[min(ki, len(k_schedule) - 1)]
-        cap = N * K
+        K = max(1, min(K, round_bytes // (MARCH_POINT_BYTES * max(n_alive, 1)), (2 ** 31 - 1) // max(n_alive, 1)))
+        cap = n_alive * K
         out_ray = torch.empty(cap, dtype=torch.int32, device=dev)
         out_step = torch.empty(cap, dtype=torch.int32, device=dev)
         out_pts = torch.empty(cap, 3, device=dev)
@@ -592,13 +605,14 @@ def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: 
         if n_pts > 0:
             with torch.no_grad():
                 raw = mlp(packer, out_pts[:n_pts], vd, 1, out_ray[:n_pts], dtype)
-            queried += n_pts
+            evaluated += n_pts
         check(L.nerf_march_composite(ptr(raw), ptr(rays), N, ptr(t_table), ptr(off), ptr(cnt), ptr(out_step), ptr(T),
                                      ptr(rgb), ptr(depth), ptr(acc), ptr(nxt), ptr(alive), ptr(exh),
-                                     float(step_size), float(t_thresh), s), "nerf_march_composite")
+                                     float(step_size), float(t_thresh), ptr(consumed), s), "nerf_march_composite")
         ki += 1
     check(L.nerf_march_finish(ptr(rgb), ptr(acc), N, int(bool(white_bkgd)), s), "nerf_march_finish")
-    return {"rgb_map_f": rgb, "depth_map_f": depth, "acc_map_f": acc, "n_queried": queried, "rounds": rounds}
+    return {"rgb_map_f": rgb, "depth_map_f": depth, "acc_map_f": acc, "n_queried": int(consumed.item()),
+            "n_evaluated": evaluated, "rounds": rounds}
 
 
 # --------------------------------------------------------------------------------------

@@ -19,6 +19,14 @@ from src.config import cfg, args  # noqa: E402
 from src.config.config import apply_gpus  # noqa: E402
 
 
+def save_grid(grid: torch.Tensor, path: str) -> None:
+    """occupancy_grid.py:72-78: torch.save of the bool [res,res,res] grid on the CPU."""
+    if grid.dtype != torch.bool or grid.dim() != 3:
+        raise ValueError(f"occupancy grid must be a 3-D bool tensor, got {grid.dtype} {tuple(grid.shape)}")
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    torch.save(grid.cpu(), path)
+
+
 def main():
     from nerf_amd import ops
     from src.models import make_network
@@ -35,11 +43,9 @@ def main():
     with torch.no_grad():
         grid = ops.bake(network.model.packer(), res, thr, bbox, dtype=network.mlp_dtype)
     name = os.path.splitext(os.path.basename(args.cfg_file))[0]
-    out_dir = os.path.join("logs", name)
-    os.makedirs(out_dir, exist_ok=True)
-    path = os.path.join(out_dir, "occupancy_grid.pt")
+    path = os.path.join("logs", name, "occupancy_grid.pt")
     print(f"Saving occupancy grid to: {path}")
-    torch.save(grid.cpu(), path)
+    save_grid(grid, path)
     print("Done.")
 
 

@@ -85,14 +85,14 @@ class Renderer:
         return all_ret
 
     # ------------------------------------------------------------------ occupancy grid
-    def load_occupancy_grid(self, grid_path):
+    def load_occupancy_grid(self, grid_path, device=None):
         """volume_renderer.py:249-259; a missing file leaves the renderer in slow mode."""
         if not os.path.exists(grid_path):
             print(f"Occupancy grid file not found: {grid_path}, run in slow mode.")
             return
         print(f"Loading occupancy grid from {grid_path}...")
         grid = torch.load(grid_path, map_location="cpu", weights_only=True)
-        self.set_occupancy_grid(grid)
+        self.set_occupancy_grid(grid, device)
         print("Occupancy grid loaded and ready for accelerated rendering.")
 
     def set_occupancy_grid(self, grid, device=None):

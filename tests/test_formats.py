@@ -1,0 +1,238 @@
+"""The drop-in's on-disk boundary: ``latest.pth``, ``occupancy_grid.pt`` and the
+blender ``transforms_{split}.json`` + RGBA PNG scene, checked on the CPU against formats the
+REFERENCE wrote (tests/golden/make_golden_ckpt.py: its save_model / make_optimizer /
+ExponentialLR / Recorder, read back with weights_only=True) and against the reference's loader
+arithmetic (blender.py:55-108).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+os.environ.setdefault("NERF_AMD_NO_ARGV", "1")
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def ckpt_golden():
+    with open(os.path.join(GOLD, "ckpt_format.json")) as f:
+        fmt = json.load(f)
+    return fmt, np.load(os.path.join(GOLD, "ckpt_samples.npz"), allow_pickle=False)
+
+
+def synthetic_grad(i, shape, step):
+    """make_golden_ckpt.synthetic_grad (exact in float64 -> float32 numpy)."""
+    n = int(np.prod(shape))
+    g = (np.sin(np.arange(n, dtype=np.float64) * 0.37 + i) * 0.05).astype(np.float32)
+    if step == 2:
+        g = g * np.float32(-0.5)
+    return g.reshape(shape)
+
+
+def reference_style_checkpoint():
+    """What the reference's train.py would save after 2 steps + 1 scheduler step, built with the
+    same objects it uses: torch.optim.Adam with one group per tensor (optimizer.py:8-28), the
+    ExponentialLR (lr_scheduler.py:68-79) and a recorder {step}; seed-0 Network."""
+    from src.config import cfg
+    from src.models.nerf.network import Network
+    from src.train.scheduler import make_lr_scheduler
+    torch.manual_seed(0)
+    net = Network()
+    lr, wd, eps = cfg.train.lr, cfg.train.weight_decay, cfg.train.eps
+    opt = torch.optim.Adam([{"params": [p], "lr": lr, "weight_decay": wd, "eps": eps} for _, p in net.named_parameters()],
+                           lr, weight_decay=wd, eps=eps)
+    sched = make_lr_scheduler(cfg, opt)
+    params = list(net.parameters())
+    for step in (1, 2):
+        for i, p in enumerate(params):
+            p.grad = torch.from_numpy(synthetic_grad(i, tuple(p.shape), step))
+        opt.step()
+    sched.step()
+    return {"net": net.state_dict(), "optim": opt.state_dict(), "scheduler": sched.state_dict(),
+            "recorder": {"step": 1000}, "epoch": 9}
+
+
+def _jsonable(x):
+    return json.loads(json.dumps(x, default=float))
+
+
+def test_checkpoint_structure_matches_reference(ckpt_golden, tmp_path):
+    """The file the drop-in would need to read, built the reference's way, is structurally
+    identical to the reference's own latest.pth and holds the same values."""
+    fmt, smp = ckpt_golden
+    ck = reference_style_checkpoint()
+    path = tmp_path / "latest.pth"
+    torch.save(ck, path)
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    assert list(ck.keys()) == fmt["top_keys"]
+    assert ck["epoch"] == fmt["epoch"] and ck["recorder"] == fmt["recorder"]
+    assert [[k, list(v.shape), str(v.dtype)] for k, v in ck["net"].items()] == [e[:3] for e in fmt["net"]]
+    assert _jsonable(ck["optim"]["param_groups"]) == fmt["optim_param_groups"]
+    for k, st in ck["optim"]["state"].items():
+        g = fmt["optim_state"][str(k)]
+        assert sorted(st.keys()) == g["keys"]
+        assert float(st["step"]) == g["step"] and torch.is_tensor(st["step"]) == g["step_is_tensor"]
+        i = int(k)
+        idx = torch.from_numpy(smp[f"idx_{i}"])
+        np.testing.assert_allclose(st["exp_avg"].reshape(-1)[idx].numpy(), smp[f"exp_avg_{i}"], rtol=1e-6, atol=0)
+        np.testing.assert_allclose(st["exp_avg_sq"].reshape(-1)[idx].numpy(), smp[f"exp_avg_sq_{i}"], rtol=1e-6,
+                                   atol=0)
+    assert _jsonable(ck["scheduler"]) == fmt["scheduler"]
+
+
+def test_reference_checkpoint_resumes_into_fused_adam_and_back(tmp_path):
+    """load_model (net_utils.py:288-320) of a reference-format latest.pth into Network + FusedAdam
+    + ExponentialLR + Recorder; save_model (net_utils.py:323-343) of that state; the re-saved file
+    loads back into torch.optim.Adam with every tensor and group unchanged."""
+    from src.config import cfg
+    from src.models.nerf.network import Network
+    from src.train.optimizer import make_optimizer
+    from src.train.recorder import Recorder
+    from src.train.scheduler import make_lr_scheduler
+    from src.utils.net_utils import load_model, save_model
+    ref = reference_style_checkpoint()
+    src_dir = tmp_path / "ref"
+    src_dir.mkdir()
+    torch.save(ref, src_dir / "latest.pth")
+    torch.manual_seed(123)  # different init: everything must come from the file
+    net = Network()
+    opt = make_optimizer(cfg, net)
+    sched = make_lr_scheduler(cfg, opt)
+    rec = Recorder(cfg)
+    begin = load_model(net, opt, sched, rec, str(src_dir), resume=True)
+    assert begin == ref["epoch"] + 1 and rec.step == 1000 and opt._step == 2
+    assert sched.last_epoch == ref["scheduler"]["last_epoch"]
+    for k, v in net.state_dict().items():
+        assert torch.equal(v, ref["net"][k]), k
+    m = torch.cat([ref["optim"]["state"][i]["exp_avg"].reshape(-1) for i in range(48)])
+    v = torch.cat([ref["optim"]["state"][i]["exp_avg_sq"].reshape(-1) for i in range(48)])
+    assert torch.equal(opt.flat_m, m) and torch.equal(opt.flat_v, v)
+    assert torch.equal(opt.flat_param, torch.cat([t.reshape(-1) for t in ref["net"].values()]))
+    out_dir = tmp_path / "ours"
+    save_model(net, opt, sched, rec, str(out_dir), 9, last=True)
+    back = torch.load(out_dir / "latest.pth", map_location="cpu", weights_only=True)
+    assert list(back.keys()) == list(ref.keys()) and back["epoch"] == 9 and back["recorder"] == ref["recorder"]
+    assert all(torch.equal(back["net"][k], ref["net"][k]) for k in ref["net"])
+    assert _jsonable(back["optim"]["param_groups"]) == _jsonable(ref["optim"]["param_groups"])
+    assert _jsonable(back["scheduler"]) == _jsonable(ref["scheduler"])
+    for i, st in ref["optim"]["state"].items():
+        b = back["optim"]["state"][i]
+        assert sorted(b.keys()) == sorted(st.keys()) and float(b["step"]) == float(st["step"])
+        assert torch.equal(b["exp_avg"], st["exp_avg"]) and torch.equal(b["exp_avg_sq"], st["exp_avg_sq"])
+    torch.manual_seed(0)
+    net2 = Network()
+    net2.load_state_dict(back["net"], strict=True)
+    adam = torch.optim.Adam([{"params": [p]} for p in net2.parameters()], lr=5e-4)
+    adam.load_state_dict(back["optim"])
+    assert torch.equal(adam.state_dict()["state"][47]["exp_avg"], ref["optim"]["state"][47]["exp_avg"])
+
+
+def test_exponential_lr_matches_reference(ckpt_golden):
+    """ExponentialLR (lr_scheduler.py:68-79): lr = 5e-4 * 0.1 ** (epoch / 500), stepped per
+    epoch, against the reference scheduler's own sequence over 1200 epochs."""
+    from src.config import cfg
+    from src.models.nerf.network import Network
+    from src.train.optimizer import make_optimizer
+    from src.train.scheduler import make_lr_scheduler
+    _, smp = ckpt_golden
+    torch.manual_seed(0)
+    net = Network()
+    opt = make_optimizer(cfg, net)
+    sched = make_lr_scheduler(cfg, opt)
+    lrs = [opt.param_groups[0]["lr"]]
+    for _ in range(1200):
+        sched.step()
+        lrs.append(opt.param_groups[0]["lr"])
+    np.testing.assert_array_equal(np.array(lrs), smp["explr_lr"])
+    assert all(g["lr"] == lrs[-1] for g in opt.param_groups)
+
+
+def test_occupancy_grid_file_roundtrip(tmp_path):
+    """occupancy_grid.py:72-78 / volume_renderer.py:249-259: a bool [res]^3 tensor written by
+    torch.save, loadable with weights_only=True; the reference's own baked lego grid file
+    format loads through Renderer.load_occupancy_grid."""
+    import occupancy_grid
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    z = np.load(os.path.join(GOLD, "lego_occupancy_grid.npz"), allow_pickle=False)
+    shape = tuple(int(v) for v in z["shape"])
+    lego = torch.from_numpy(np.unpackbits(z["packed"])[: int(np.prod(shape))].reshape(shape).astype(bool))
+    path = str(tmp_path / "logs" / "lego" / "occupancy_grid.pt")
+    occupancy_grid.save_grid(lego, path)
+    g = torch.load(path, weights_only=True)
+    assert g.dtype == torch.bool and tuple(g.shape) == (128, 128, 128) and torch.equal(g, lego)
+    import hashlib
+    assert hashlib.sha256(g.numpy().tobytes()).hexdigest() == str(z["sha256"])
+    with pytest.raises(ValueError):
+        occupancy_grid.save_grid(lego.to(torch.uint8), path)
+    r = Renderer(None)
+    r.load_occupancy_grid(path, device="cpu")
+    assert torch.equal(r.occupancy_grid, lego) and r.resolution == 128
+    r2 = Renderer(None)
+    r2.load_occupancy_grid(str(tmp_path / "missing.pt"), device="cpu")  # silently stays in slow mode
+    assert r2.occupancy_grid is None
+
+
+def write_blender_scene(root, n=3, H=6, W=8, seed=0):
+    """A tiny transforms_train.json + RGBA PNG scene in the blender layout (blender.py:55-97)."""
+    from PIL import Image
+    from src.utils.camera import pose_spherical
+    rng = np.random.default_rng(seed)
+    scene = root / "lego"
+    (scene / "train").mkdir(parents=True)
+    frames, rgba = [], []
+    for k in range(n):
+        a = rng.integers(0, 256, size=(H, W, 4), dtype=np.uint8)
+        a[0, 0, 3], a[0, 1, 3] = 0, 255  # fully transparent and fully opaque pixels
+        Image.fromarray(a, "RGBA").save(scene / "train" / f"r_{k}.png")
+        rgba.append(a)
+        frames.append({"file_path": f"./train/r_{k}", "rotation": 0.0,
+                       "transform_matrix": pose_spherical(-180.0 + 120.0 * k, -30.0, 4.0).tolist()})
+    meta = {"camera_angle_x": 0.6911112070083618, "frames": frames}
+    with open(scene / "transforms_train.json", "w") as f:
+        json.dump(meta, f)
+    return meta, rgba
+
+
+def reference_loader_arithmetic(meta, rgba, W):
+    """blender.py:74-97 restated: (uint8 / 255.) in float64 -> float32, white compositing in
+    float32, pose as float32, focal in float64."""
+    imgs = []
+    for a in rgba:
+        img = (np.array(a) / 255.).astype(np.float32)
+        img = img[..., :3] * img[..., -1:] + (1. - img[..., -1:])
+        imgs.append(img)
+    poses = [torch.tensor(fr["transform_matrix"], dtype=torch.float32).numpy() for fr in meta["frames"]]
+    focal = .5 * W / np.tan(.5 * float(meta["camera_angle_x"]))
+    return np.stack(imgs), np.stack(poses), focal
+
+
+@pytest.mark.parametrize("cams", [[0, -1, 1], [1, -1, 1]])
+def test_blender_loader_matches_reference_arithmetic(tmp_path, cams):
+    from src.datasets.nerf.blender import Dataset
+    meta, rgba = write_blender_scene(tmp_path)
+    ds = Dataset(data_root=str(tmp_path), split="train", cams=cams, H=6, W=8, input_ratio=1.0, device="cpu")
+    imgs, poses, focal = reference_loader_arithmetic(meta, rgba, 8)
+    sel = slice(cams[0], None, cams[2])
+    np.testing.assert_array_equal(ds.images.numpy(), imgs[sel])
+    np.testing.assert_array_equal(ds.poses.numpy(), poses[sel])
+    assert ds.focal == focal and (ds.H, ds.W) == (6, 8)
+    assert float(ds.images[0, 0, 0, 0]) == 1.0  # transparent -> white
+
+
+@pytest.mark.gpu
+def test_blender_loader_rays_on_gpu(tmp_path, cuda):
+    """The loader's on-GPU ray table (nerf_raygen on pixel ids) against the oracle's get_rays
+    (blender.py:13-32) for every pixel of every image, and the rgb gather."""
+    from oracle import nerf_oracle as O
+    from src.datasets.nerf.blender import Dataset
+    meta, rgba = write_blender_scene(tmp_path, H=12, W=16)
+    ds = Dataset(data_root=str(tmp_path), split="train", cams=[0, -1, 1], H=12, W=16, device=cuda)
+    imgs, poses, focal = reference_loader_arithmetic(meta, rgba, 16)
+    for k in range(3):
+        rays, rgbs = ds.image_rays(k)
+        o, d = O.get_rays(12, 16, focal, torch.from_numpy(poses[k]))
+        np.testing.assert_array_equal(rays[:, :3].cpu().numpy(), o.reshape(-1, 3).numpy())
+        np.testing.assert_allclose(rays[:, 3:].cpu().numpy(), d.reshape(-1, 3).numpy(), rtol=0, atol=2e-7)
+        np.testing.assert_array_equal(rgbs.cpu().numpy(), imgs[k].reshape(-1, 3))
