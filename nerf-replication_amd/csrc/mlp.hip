@@ -1037,13 +1037,15 @@ __host__ __device__ constexpr int dw_job_tiles(int j) { return dw_job_desc(j).nd
 template <class P> __host__ __device__ constexpr int dw_nbuf() { return P::CH == 2 ? NERF_DW_NBUF_BF16 : 2; }
 __host__ __device__ constexpr int perm_row(int i) { return acc_row(i & 15, i >> 4); }
 
-// work items: item_off[j] = first item of job j (item_off[NDWJOB] = total)
+// work items: segment s = items [item_off[s], item_off[s + 1]) of job job_of[s]
+// (item_off[NDWJOB] = total); segments are ordered longest item first
 struct DwArgs {
   const void* dz;
   const void* act;
   int64_t nblk;       // 32-sample blocks in the stores
   float* grad;        // flat [NET_PARAMS], accumulated
   int item_off[NDWJOB + 1];
+  int job_of[NDWJOB];
 };
 
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n in [0, 63] (n is a multiple of G here)
@@ -1359,10 +1361,11 @@ __global__ void __launch_bounds__(DW_WAVES * 64) dw_kernel(DwArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
   char* lds = (char*)smem_u4;
   const int item = blockIdx.x;
-  int j = 0;
+  int seg = 0;
 #pragma unroll
-  for (int k = 1; k < NDWJOB; ++k) j += a.item_off[k] <= item ? 1 : 0;
-  const int n_items = a.item_off[j + 1] - a.item_off[j], i = item - a.item_off[j];
+  for (int k = 1; k < NDWJOB; ++k) seg += a.item_off[k] <= item ? 1 : 0;
+  const int n_items = a.item_off[seg + 1] - a.item_off[seg], i = item - a.item_off[seg];
+  const int j = a.job_of[seg];
   const int64_t b_begin = a.nblk * i / n_items, b_end = a.nblk * (i + 1) / n_items;
   switch (j) {
     case 0: dw_job<P, 0>(a, b_begin, b_end, lds); break;
@@ -1496,18 +1499,32 @@ static int cu_count() {
     n = 256;
   return n;
 }
-// cost of one 32-sample block of job j: bf16 dW is HBM-bound (tile-blocks streamed), fp32 dW
-// is MFMA-bound (MFMAs of the job's busiest wave per K step: k-tiles, + the alpha row for
-// feature/alpha, 9 for the view layer's waves 0..3)
+// cost (SIMD cycles) of one 32-sample block of job j.  bf16 dW is HBM-bound and its 4-deep
+// ring hides the fetch latency: the tile-blocks streamed.  fp32 dW: the busiest wave pair's
+// MFMAs (2 waves x 16 K steps x (k-tiles, + the alpha row for feature/alpha, 9 for the view
+// layer's waves 0..3) x 64 cycles), or -- for the light L0 job, behind a 2-deep ring -- the
+// block's fetch: its latency + its bytes at a CU's share of HBM (~25 GB/s, 393 cycles per
+// 4 KiB tile).
 #ifndef NERF_DW_BALANCE_MFMA
-#define NERF_DW_BALANCE_MFMA 0  /* measured: byte-balanced items are 2 % faster in fp32 too */
+#define NERF_DW_BALANCE_MFMA 1
 #endif
-static int dw_job_cost(int dtype, int j) {
+#ifndef NERF_DW_LAT_CYCLES
+#define NERF_DW_LAT_CYCLES 4000
+#endif
+// fp32: two items per CU (measured -2.5 % over one: the tail of the last items is shorter);
+// bf16: one (every extra item re-adds its partial dW with atomics)
+#ifndef NERF_DW_ITEMS_PER_CU
+#define NERF_DW_ITEMS_PER_CU 2
+#endif
+static int64_t dw_job_cost(int dtype, int j) {
   if (dtype != 0 || !NERF_DW_BALANCE_MFMA) return dw_job_tiles(j);
-  return j < 8 ? gemm_k_tiles(j) : 9;
+  const int64_t mfma = 2 * 16 * (j < 8 ? gemm_k_tiles(j) : 9) * 64;
+  const int64_t fetch = NERF_DW_LAT_CYCLES + 393 * (int64_t)dw_job_tiles(j);
+  return mfma > fetch ? mfma : fetch;
 }
-static void dw_items(int dtype, int64_t nblk, int item_off[NDWJOB + 1]) {
-  static const int target = cu_count();
+static void dw_items(int dtype, int64_t nblk, int item_off[NDWJOB + 1], int job_of[NDWJOB]) {
+  static const int cus = cu_count();
+  const int target = cus * (dtype == 0 ? NERF_DW_ITEMS_PER_CU : 1);
   int n[NDWJOB];
   int64_t cost = 0;
   for (int j = 0; j < NDWJOB; ++j) cost += dw_job_cost(dtype, j);
@@ -1520,7 +1537,7 @@ static void dw_items(int dtype, int64_t nblk, int item_off[NDWJOB + 1]) {
   // the remaining CUs go, one at a time, to the job whose items are the longest
   while (total < target) {
     int best = -1;
-    double worst = 0.0;
+    double worst = 0.0;  // (worst = 0 only before the first candidate)
     for (int j = 0; j < NDWJOB; ++j) {
       if (n[j] >= nblk) continue;
       const double per = (double)dw_job_cost(dtype, j) / n[j];
@@ -1530,12 +1547,21 @@ static void dw_items(int dtype, int64_t nblk, int item_off[NDWJOB + 1]) {
     ++n[best];
     ++total;
   }
+  // longest items first: with more items than CUs, the short ones fill the tail
+  for (int j = 0; j < NDWJOB; ++j) job_of[j] = j;
+  for (int a = 0; a < NDWJOB; ++a)
+    for (int b = a + 1; b < NDWJOB; ++b)
+      if ((double)dw_job_cost(dtype, job_of[b]) / n[job_of[b]] > (double)dw_job_cost(dtype, job_of[a]) / n[job_of[a]]) {
+        const int t = job_of[a];
+        job_of[a] = job_of[b];
+        job_of[b] = t;
+      }
   item_off[0] = 0;
-  for (int j = 0; j < NDWJOB; ++j) item_off[j + 1] = item_off[j] + n[j];
+  for (int s = 0; s < NDWJOB; ++s) item_off[s + 1] = item_off[s] + n[job_of[s]];
 }
 int64_t nerf_mlp_dw_items(int dtype, int64_t M) {
-  int off[NDWJOB + 1];
-  dw_items(dtype, nerf_mlp_padded_samples(M) / 32, off);
+  int off[NDWJOB + 1], job[NDWJOB];
+  dw_items(dtype, nerf_mlp_padded_samples(M) / 32, off, job);
   return off[NDWJOB];
 }
 
@@ -1561,7 +1587,7 @@ int nerf_mlp_bwd_dw(int dtype, int64_t M, const void* act, const void* dz, float
   NERF_REQUIRE(act && dz && grad, "nerf_mlp_bwd_dw: null pointer");
   const int64_t nblk = nerf_mlp_padded_samples(M) / 32;
   DwArgs w{dz, act, nblk, grad, {}};
-  dw_items(dtype, nblk, w.item_off);
+  dw_items(dtype, nblk, w.item_off, w.job_of);
   dim3 grid((unsigned)w.item_off[NDWJOB]);
   if (dtype == 0) {
     allow_lds(dw_kernel<PF32>, dw_lds_bytes<PF32>());
