@@ -136,6 +136,12 @@ int nerf_grid_index(const float* pts, int64_t M, const float* bbox_host, int res
 int64_t nerf_bake_num_points(int res, int dedup);
 int nerf_bake_points(int res, const float* bbox_host, int dedup, float* pts, hipStream_t stream);
 int nerf_bake_reduce(const float* raw, int res, int dedup, float threshold, uint8_t* grid, hipStream_t stream);
+/* The same for the voxel slab x in [x0, x1) only (one slab per rank, the bool
+ * grid all-gathered afterwards); grid is the slab [x1-x0][res][res]. */
+int64_t nerf_bake_num_points_slab(int res, int dedup, int x0, int x1);
+int nerf_bake_points_slab(int res, const float* bbox_host, int dedup, int x0, int x1, float* pts, hipStream_t stream);
+int nerf_bake_reduce_slab(const float* raw, int res, int dedup, int x0, int x1, float threshold, uint8_t* grid,
+                          hipStream_t stream);
 
 /* ---- (a12) grid-accelerated march (render_accelerated, volume_renderer.py:268-357) --------------
  * Round structure: init; repeat { zero counters; gather (<= K occupied steps per alive ray,

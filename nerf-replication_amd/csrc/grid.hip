@@ -51,10 +51,13 @@ __global__ void grid_index_kernel(GridIndexArgs a) {
 // ------------------------------------------------------------------------------------
 // bake
 // ------------------------------------------------------------------------------------
+// A bake covers the voxel slab x in [x0, x1) (the whole grid: [0, res)); point and grid
+// indices are slab-relative.
 struct BakeArgs {
   int res;
   BBox bb;
-  int dedup;   // 1: (res+1)^3 lattice points; 0: res^3 x 8 corners
+  int dedup;   // 1: (x1-x0+1)(res+1)^2 lattice points; 0: (x1-x0) res^2 x 8 corners
+  int x0, x1;
   float* pts;
 };
 
@@ -64,19 +67,20 @@ __device__ __forceinline__ float voxel_size(const BBox& bb, int k, int res) {
 
 __global__ void bake_points_kernel(BakeArgs a) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nx = a.x1 - a.x0;
   if (a.dedup) {
     const int64_t n = (int64_t)(a.res + 1);
-    if (i >= n * n * n) return;
-    const int L[3] = {(int)(i / (n * n)), (int)((i / n) % n), (int)(i % n)};
+    if (i >= (nx + 1) * n * n) return;
+    const int L[3] = {a.x0 + (int)(i / (n * n)), (int)((i / n) % n), (int)(i % n)};
 #pragma unroll
     for (int k = 0; k < 3; ++k)
       a.pts[i * 3 + k] = fadd(a.bb.mn[k], fmul((float)L[k], voxel_size(a.bb, k, a.res)));
   } else {
     const int64_t n = (int64_t)a.res;
-    if (i >= n * n * n * 8) return;
+    if (i >= nx * n * n * 8) return;
     const int64_t v = i >> 3;
     const int c = (int)(i & 7);  // meshgrid 'ij' over the 2x2x2 corner offsets
-    const int idx[3] = {(int)(v / (n * n)), (int)((v / n) % n), (int)(v % n)};
+    const int idx[3] = {a.x0 + (int)(v / (n * n)), (int)((v / n) % n), (int)(v % n)};
     const int off[3] = {(c >> 2) & 1, (c >> 1) & 1, c & 1};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -88,16 +92,17 @@ __global__ void bake_points_kernel(BakeArgs a) {
 }
 
 struct BakeReduceArgs {
-  const float* raw;  // [P,4]
+  const float* raw;  // [P,4] (slab points)
   int res, dedup;
+  int x0, x1;
   float threshold;
-  uint8_t* grid;     // [res^3]
+  uint8_t* grid;     // [x1 - x0][res][res]
 };
 
 __global__ void bake_reduce_kernel(BakeReduceArgs a) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = a.res;
-  if (v >= n * n * n) return;
+  if (v >= (int64_t)(a.x1 - a.x0) * n * n) return;
   const int x = (int)(v / (n * n)), y = (int)((v / n) % n), z = (int)(v % n);
   bool occ = false;
 #pragma unroll
@@ -355,23 +360,39 @@ int nerf_grid_index(const float* pts, int64_t M, const float* bbox_host, int res
   return check_launch("nerf_grid_index");
 }
 
-int64_t nerf_bake_num_points(int res, int dedup) {
-  const int64_t n = res;
-  return dedup ? (n + 1) * (n + 1) * (n + 1) : n * n * n * 8;
+int64_t nerf_bake_num_points_slab(int res, int dedup, int x0, int x1) {
+  const int64_t n = res, nx = x1 - x0;
+  if (res <= 0 || x0 < 0 || x1 > res || nx < 0) return -1;
+  if (nx == 0) return 0;
+  return dedup ? (nx + 1) * (n + 1) * (n + 1) : nx * n * n * 8;
 }
+int64_t nerf_bake_num_points(int res, int dedup) { return nerf_bake_num_points_slab(res, dedup, 0, res); }
 
-int nerf_bake_points(int res, const float* bbox_host, int dedup, float* pts, hipStream_t stream) {
-  NERF_REQUIRE(res > 0 && bbox_host && pts, "nerf_bake_points: bad arguments");
-  BakeArgs a{res, make_bbox(bbox_host), dedup, pts};
-  hipLaunchKernelGGL(bake_points_kernel, grid1(nerf_bake_num_points(res, dedup)), dim3(256), 0, stream, a);
+int nerf_bake_points_slab(int res, const float* bbox_host, int dedup, int x0, int x1, float* pts,
+                          hipStream_t stream) {
+  NERF_REQUIRE(res > 0 && bbox_host && 0 <= x0 && x0 <= x1 && x1 <= res, "nerf_bake_points: bad arguments");
+  if (x0 == x1) return 0;
+  NERF_REQUIRE(pts, "nerf_bake_points: null pointer");
+  BakeArgs a{res, make_bbox(bbox_host), dedup, x0, x1, pts};
+  hipLaunchKernelGGL(bake_points_kernel, grid1(nerf_bake_num_points_slab(res, dedup, x0, x1)), dim3(256), 0, stream,
+                     a);
   return check_launch("nerf_bake_points");
 }
+int nerf_bake_points(int res, const float* bbox_host, int dedup, float* pts, hipStream_t stream) {
+  return nerf_bake_points_slab(res, bbox_host, dedup, 0, res, pts, stream);
+}
 
-int nerf_bake_reduce(const float* raw, int res, int dedup, float threshold, uint8_t* grid, hipStream_t stream) {
-  NERF_REQUIRE(res > 0 && raw && grid, "nerf_bake_reduce: bad arguments");
-  BakeReduceArgs a{raw, res, dedup, threshold, grid};
-  hipLaunchKernelGGL(bake_reduce_kernel, grid1((int64_t)res * res * res), dim3(256), 0, stream, a);
+int nerf_bake_reduce_slab(const float* raw, int res, int dedup, int x0, int x1, float threshold, uint8_t* grid,
+                          hipStream_t stream) {
+  NERF_REQUIRE(res > 0 && 0 <= x0 && x0 <= x1 && x1 <= res, "nerf_bake_reduce: bad arguments");
+  if (x0 == x1) return 0;
+  NERF_REQUIRE(raw && grid, "nerf_bake_reduce: null pointer");
+  BakeReduceArgs a{raw, res, dedup, x0, x1, threshold, grid};
+  hipLaunchKernelGGL(bake_reduce_kernel, grid1((int64_t)(x1 - x0) * res * res), dim3(256), 0, stream, a);
   return check_launch("nerf_bake_reduce");
+}
+int nerf_bake_reduce(const float* raw, int res, int dedup, float threshold, uint8_t* grid, hipStream_t stream) {
+  return nerf_bake_reduce_slab(raw, res, dedup, 0, res, threshold, grid, stream);
 }
 
 // state: T, rgb[3], depth, acc (f32) ; next_step (i32) ; alive, exhausted (u8)

@@ -49,6 +49,9 @@ SIGNATURES = {
     "nerf_bake_num_points": (_i64, [_i32, _i32]),
     "nerf_bake_points": (_i32, [_i32, _p, _i32, _p, _p]),
     "nerf_bake_reduce": (_i32, [_p, _i32, _i32, _f32, _p, _p]),
+    "nerf_bake_num_points_slab": (_i64, [_i32, _i32, _i32, _i32]),
+    "nerf_bake_points_slab": (_i32, [_i32, _p, _i32, _i32, _i32, _p, _p]),
+    "nerf_bake_reduce_slab": (_i32, [_p, _i32, _i32, _i32, _i32, _f32, _p, _p]),
     "nerf_march_init": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "nerf_march_gather": (_i32, [_p, _i64, _p, _i32, _p, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _p,
                                  _p, _p, _p, _p, _p, _p, _i64, _p]),

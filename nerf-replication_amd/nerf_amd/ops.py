@@ -523,19 +523,27 @@ def bake_lattice_exact(res: int, bbox=SCENE_BBOX) -> bool:
 
 
 def bake(packer: PackedMLP, res: int, threshold: float, bbox=SCENE_BBOX, dtype=F32, device=None,
-         dedup: Optional[bool] = None, return_sigma: bool = False):
-    """Occupancy grid bake -> bool [res,res,res] (occupancy_grid.py:15-80)."""
+         dedup: Optional[bool] = None, return_sigma: bool = False, slab=None):
+    """Occupancy grid bake -> bool [res,res,res] (occupancy_grid.py:15-80); with slab=(x0, x1)
+    only the voxels x0 <= ix < x1 -> bool [x1-x0,res,res] (one rank's share)."""
     device = device or packer.params[0].device
     if dedup is None:
         dedup = bake_lattice_exact(res, bbox)
-    P = lib().nerf_bake_num_points(res, int(dedup))
+    x0, x1 = (0, res) if slab is None else (int(slab[0]), int(slab[1]))
+    L = lib()
+    P = L.nerf_bake_num_points_slab(res, int(dedup), x0, x1)
+    if P < 0:
+        raise ValueError(f"bake: bad slab {(x0, x1)} for res {res}")
+    grid = torch.zeros(x1 - x0, res, res, device=device, dtype=torch.uint8)
+    if P == 0:
+        return grid.bool()
     pts = torch.empty(P, 3, device=device, dtype=torch.float32)
     s = stream_of(pts)
-    check(lib().nerf_bake_points(res, _bbox_arr(bbox), int(dedup), ptr(pts), s), "nerf_bake_points")
+    check(L.nerf_bake_points_slab(res, _bbox_arr(bbox), int(dedup), x0, x1, ptr(pts), s), "nerf_bake_points")
     with torch.no_grad():
         raw = mlp(packer, pts, None, 1, None, dtype, density_only=True)
-    grid = torch.empty(res, res, res, device=device, dtype=torch.uint8)
-    check(lib().nerf_bake_reduce(ptr(raw), res, int(dedup), float(threshold), ptr(grid), s), "nerf_bake_reduce")
+    check(L.nerf_bake_reduce_slab(ptr(raw), res, int(dedup), x0, x1, float(threshold), ptr(grid), s),
+          "nerf_bake_reduce")
     if return_sigma:
         return grid.bool(), raw[:, 3].clamp_min(0), pts
     return grid.bool()

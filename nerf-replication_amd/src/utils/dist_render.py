@@ -1,6 +1,7 @@
 """Multi-GPU inference: one image's rays split into contiguous row blocks, one per rank,
 rendered independently, then gathered (640,000 rays / 8 = 80,000 per GPU;
-rgb/depth/acc gathered at the end, no other collective).
+rgb/depth/acc gathered at the end, no other collective).  The grid bake likewise: one voxel
+slab per rank (16 x 128 x 128 at 8 ranks), then an all-gather of the bool grid (2 MB).
 
 Used by run.py --type evaluate|network under torch.distributed.run; the renderer is any
 object with render / render_accelerated (the reference's Renderer interface)."""
@@ -55,3 +56,23 @@ def render_distributed(renderer, batch, accelerated: bool = False, keys=None):
         else:
             res[k] = v
     return res
+
+
+def bake_distributed(bake_slab, res: int):
+    """Occupancy bake split into x-slabs: rank r bakes voxels shard_bounds(res, r, W) with
+    ``bake_slab((x0, x1)) -> bool [x1-x0, res, res]``; the slabs are all-gathered (uint8,
+    padded to the largest share) so every rank returns the full bool [res, res, res] grid."""
+    world = _world()
+    if world == 1:
+        return bake_slab((0, res))
+    rank = dist.get_rank()
+    a, b = shard_bounds(res, rank, world)
+    part = bake_slab((a, b)).to(torch.uint8)
+    share = (res + world - 1) // world
+    pad = torch.zeros((share, res, res), dtype=torch.uint8, device=part.device)
+    pad[: b - a] = part
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    out = torch.cat([parts[r][: shard_bounds(res, r, world)[1] - shard_bounds(res, r, world)[0]]
+                     for r in range(world)], 0)
+    return out.bool()

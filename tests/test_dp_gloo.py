@@ -129,3 +129,52 @@ def test_two_rank_gradient_average_and_broadcast():
         assert render_ok  # tile-split render == single-process render
         assert two_chunk_ok  # one bucket per net after its last chunk; == the flat average
         assert seeds_distinct  # every rank draws its own rays
+
+
+def _fake_bake_slab(res):
+    """A deterministic 'bake' of voxel slab (x0, x1): cell (x, y, z) occupied iff (7x + 3y + z) % 5 == 0."""
+    def f(slab):
+        x0, x1 = slab
+        x, y, z = torch.meshgrid(torch.arange(x0, x1), torch.arange(res), torch.arange(res), indexing="ij")
+        return (7 * x + 3 * y + z) % 5 == 0
+    return f
+
+
+def _bake_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      NERF_AMD_NO_ARGV="1")
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "nerf-replication_amd")]
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from src.utils.dist_render import bake_distributed, shard_bounds
+    res = 10
+    seen = []
+    fake = _fake_bake_slab(res)
+
+    def slab(sl):
+        seen.append(tuple(sl))
+        return fake(sl)
+    got = bake_distributed(slab, res)
+    full = fake((0, res))
+    q.put((rank, bool(torch.equal(got, full)), seen, shard_bounds(res, rank, world)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_grid_bake_voxel_slabs_all_gathered(world):
+    """SURVEY.md 8e grid bake: each rank bakes only its own x-slab (sizes differ by at most one;
+    res 10 over 3 ranks pads the all-gather), and every rank ends with the full grid."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bake_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, seen, bounds in res:
+        assert ok
+        assert seen == [tuple(bounds)]  # the rank baked its own slab and nothing else
