@@ -293,8 +293,64 @@ def grid_times(cfg, net, ds, device, reps=2):
                 times.append(time.perf_counter() - t0)
         out["march_s_per_frame"] = round(min(times), 4)
         out["march_queried_points"] = int(o["n_queried"])
-        if "n_evaluated" in o:
-            out["march_evaluated_points"] = int(o["n_evaluated"])
+        out["march_evaluated_points"] = int(o["n_evaluated"])
+        out["trained"] = trained_grid_times(cfg, device, reps)
+    return out
+
+
+def trained_grid_times(cfg, device, reps=2):
+    """Config 4 on a net where the bake threshold bites and rays terminate: the fixture weights
+    trained on the procedural scene (tests/golden/trained_v2.npz, tools/train_teacher.py), its
+    own res-128 bake (occupancy_grid.py), then the grid march of an 800x800 held-out view."""
+    import contextlib
+    import io
+    import numpy as np
+    from nerf_amd import ops
+    from src.datasets.nerf.synthetic import view_poses
+    from src.models import make_network
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    from src.utils.camera import focal_for
+    z = np.load(os.path.join(ROOT, "tests", "golden", "trained_v2.npz"), allow_pickle=False)
+    torch.manual_seed(0)
+    net = make_network(cfg)
+    net.load_state_dict({k: torch.from_numpy(z[k]) for k in z.files}, strict=True)
+    net = net.to(device).eval()
+    out = {}
+    with torch.no_grad():
+        ops.bake(net.model.packer(), 128, 1.0, dtype=cfg.task_arg.mlp_dtype)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            grid = ops.bake(net.model.packer(), 128, 1.0, dtype=cfg.task_arg.mlp_dtype)
+        torch.cuda.synchronize()
+        out["bake_s"] = round((time.perf_counter() - t0) / reps, 4)
+        out["bake_occupied"] = int(grid.sum())
+        r = Renderer(net)
+        r.set_occupancy_grid(grid, device)
+        pose = view_poses(2, seed=1)[0].to(device)
+        pix = torch.arange(800 * 800, device=device)
+        rays, _, _ = ops.raygen(pose.reshape(1, 4, 4), 800, 800, focal_for(800), pix=pix)
+        batch = {"rays": rays, "near": ops.device_scalar(2.0, device), "far": ops.device_scalar(6.0, device)}
+        with contextlib.redirect_stdout(io.StringIO()):
+            r.render_accelerated(batch)
+            times = []
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                o = r.render_accelerated(batch)
+                torch.cuda.synchronize()
+                times.append(time.perf_counter() - t0)
+            cfg.task_arg.perturb = 0
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r.render(batch)
+            torch.cuda.synchronize()
+            out["hierarchical_render_s"] = round(time.perf_counter() - t0, 4)
+            cfg.task_arg.perturb = 1
+    out["march_s_per_frame"] = round(min(times), 4)
+    out["march_queried_points"] = int(o["n_queried"])
+    out["march_evaluated_points"] = int(o["n_evaluated"])
+    out["march_rounds"] = int(o.get("rounds", 0))
     return out
 
 

@@ -145,7 +145,7 @@ int nerf_bake_reduce_slab(const float* raw, int res, int dedup, int x0, int x1, 
 
 /* ---- (a12) grid-accelerated march (render_accelerated, volume_renderer.py:268-357) --------------
  * Round structure: init; repeat { zero counters; gather (<= K occupied steps per alive ray,
- * compacted points; cap = room for points, K <= cap <= INT32_MAX -- size it alive rays x K, a ray
+ * compacted points; a ray whose T < t_split gathers at most k_low; cap = room for points, K <= cap <= INT32_MAX -- size it alive rays x K, a ray
  * that finds no room keeps its position for the next round); fine MLP on the points; composite
  * (stops at T < t_thresh; consumed (nullable, uint64) += the points composited, i.e. the
  * reference's MLP queries -- points gathered past a ray's termination are dropped) } until no
@@ -153,7 +153,8 @@ int nerf_bake_reduce_slab(const float* raw, int res, int dedup, int x0, int x1, 
 int nerf_march_init(float* T, float* rgb, float* depth, float* acc, int32_t* next_step, uint8_t* alive,
                     uint8_t* exhausted, int64_t N, hipStream_t stream);
 int nerf_march_gather(const float* rays, int64_t N, const float* t_table, int n_steps, const uint8_t* grid, int res,
-                      const float* bbox_host, int K, float* T, float* rgb, float* depth, float* acc,
+                      const float* bbox_host, int K, int k_low, float t_split, float* T, float* rgb, float* depth,
+                      float* acc,
                       int32_t* next_step, uint8_t* alive, uint8_t* exhausted, int32_t* counters,
                       int32_t* start_step_scratch, int32_t* out_ray, int32_t* out_step, float* out_pts,
                       int32_t* ray_off, int32_t* ray_cnt, int64_t cap, hipStream_t stream);

@@ -143,6 +143,8 @@ struct MarchGatherArgs {
   int res;
   BBox bb;
   int K;
+  int k_low;       // rays with T < t_split gather at most k_low steps (they terminate soon)
+  float t_split;
   MarchState st;
   int32_t* counters;   // [0] points written, [1] rays alive after gather
   int32_t* out_ray;    // [cap]
@@ -170,7 +172,11 @@ __global__ void march_gather_kernel(MarchGatherArgs a) {
   const float* ray = a.rays + (in ? r : 0) * 6;
   float p[3];
   if (live) {
-    for (; s < a.n_steps && cnt < a.K; ++s)
+    // a ray whose transmittance has already dropped is near its termination step: gathering
+    // few steps for it wastes fewer speculative MLP evaluations (outputs are unchanged -- the
+    // compositor stops where the reference does, and an unfinished ray gathers again)
+    const int k = a.st.T[r] < a.t_split ? (a.k_low < a.K ? a.k_low : a.K) : a.K;
+    for (; s < a.n_steps && cnt < k; ++s)
       if (march_occupied(a, ray, a.t_table[s], p)) ++cnt;
   }
   // wave-aggregated reservation
@@ -408,14 +414,16 @@ int nerf_march_init(float* T, float* rgb, float* depth, float* acc, int32_t* nex
 // counters[0] = points emitted, counters[1] = rays alive entering this round (zero them first).
 // start_step_scratch: [N] int32 workspace.
 int nerf_march_gather(const float* rays, int64_t N, const float* t_table, int n_steps, const uint8_t* grid, int res,
-                      const float* bbox_host, int K, float* T, float* rgb, float* depth, float* acc,
+                      const float* bbox_host, int K, int k_low, float t_split, float* T, float* rgb, float* depth,
+                      float* acc,
                       int32_t* next_step, uint8_t* alive, uint8_t* exhausted, int32_t* counters,
                       int32_t* start_step_scratch, int32_t* out_ray, int32_t* out_step, float* out_pts,
                       int32_t* ray_off, int32_t* ray_cnt, int64_t cap, hipStream_t stream) {
   NERF_REQUIRE(N >= 0 && n_steps >= 0 && K > 0 && res > 1 && bbox_host, "nerf_march_gather: bad arguments");
   NERF_REQUIRE(cap >= K && cap <= INT32_MAX, "nerf_march_gather: need K <= cap <= INT32_MAX (point offsets are int32)");
   if (N == 0) return 0;
-  MarchGatherArgs a{rays, N, t_table, n_steps, grid, res, make_bbox(bbox_host), K,
+  NERF_REQUIRE(k_low > 0, "nerf_march_gather: k_low must be > 0");
+  MarchGatherArgs a{rays, N, t_table, n_steps, grid, res, make_bbox(bbox_host), K, k_low, t_split,
                     {T, rgb, depth, acc, next_step, alive, exhausted},
                     counters, out_ray, out_step, out_pts, ray_off, ray_cnt, cap};
   if (hipMemcpyAsync(start_step_scratch, next_step, N * sizeof(int32_t), hipMemcpyDeviceToDevice, stream) !=

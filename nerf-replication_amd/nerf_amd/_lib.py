@@ -53,8 +53,8 @@ SIGNATURES = {
     "nerf_bake_points_slab": (_i32, [_i32, _p, _i32, _i32, _i32, _p, _p]),
     "nerf_bake_reduce_slab": (_i32, [_p, _i32, _i32, _i32, _i32, _f32, _p, _p]),
     "nerf_march_init": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _p]),
-    "nerf_march_gather": (_i32, [_p, _i64, _p, _i32, _p, _i32, _p, _i32, _p, _p, _p, _p, _p, _p, _p, _p,
-                                 _p, _p, _p, _p, _p, _p, _i64, _p]),
+    "nerf_march_gather": (_i32, [_p, _i64, _p, _i32, _p, _i32, _p, _i32, _i32, _f32, _p, _p, _p, _p, _p, _p, _p,
+                                 _p, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "nerf_march_composite": (_i32, [_p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _f32, _f32, _p, _p]),
     "nerf_march_finish": (_i32, [_p, _p, _i64, _i32, _p]),
     "nerf_metrics_workspace_bytes": (_i64, [_i32, _i32]),

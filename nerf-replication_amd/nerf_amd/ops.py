@@ -554,14 +554,17 @@ MARCH_POINT_BYTES = 4 + 4 + 12 + 16  # out_ray, out_step, out_pts, raw per gathe
 
 def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: torch.Tensor, step_size: float = 0.005,
           t_thresh: float = 1e-4, bbox=SCENE_BBOX, white_bkgd: bool = True, dtype=F32,
-          t_table: Optional[torch.Tensor] = None, k_schedule=(16, 32, 64, 128, 256, 512, 1024),
-          round_bytes: int = 1 << 31):
+          t_table: Optional[torch.Tensor] = None, k_schedule=(12, 24, 48, 96, 192, 384, 768),
+          round_bytes: int = 1 << 31, k_low: int = 8, t_split: float = 0.9):
     """Grid-accelerated march with early termination -> dict(rgb_map_f, depth_map_f,
     acc_map_f, n_queried, n_evaluated, rounds).
 
     Each round gathers up to K occupied steps of every alive ray and evaluates them in one MLP
     launch; compositing stops at T < t_thresh, so points past a ray's termination were
-    evaluated speculatively.  n_queried counts the composited points only -- exactly the
+    evaluated speculatively; a ray whose transmittance is already below t_split gathers at most
+    k_low steps (it is about to terminate; on the trained fixture net's 800x800 view this cut the
+    speculative evaluations from 48 % to 6 % of the queries and the frame from 0.166 to 0.127 s,
+    profiles/r2/march_sweep.json).  n_queried counts the composited points only -- exactly the
     reference's MLP queries (volume_renderer.py:324) -- and n_evaluated every point the MLP ran
     on.  A round's point buffers are sized alive rays x K, with K capped so they stay within
     round_bytes (and int32 offsets)."""
@@ -601,7 +604,8 @@ def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: 
         out_step = torch.empty(cap, dtype=torch.int32, device=dev)
         out_pts = torch.empty(cap, 3, device=dev)
         counters.zero_()
-        check(L.nerf_march_gather(ptr(rays), N, ptr(t_table), n_steps, ptr(g), res, bb, K, ptr(T), ptr(rgb),
+        check(L.nerf_march_gather(ptr(rays), N, ptr(t_table), n_steps, ptr(g), res, bb, K, int(k_low), float(t_split),
+                                  ptr(T), ptr(rgb),
                                   ptr(depth), ptr(acc), ptr(nxt), ptr(alive), ptr(exh), ptr(counters), ptr(start),
                                   ptr(out_ray), ptr(out_step), ptr(out_pts), ptr(off), ptr(cnt), cap, s),
               "nerf_march_gather")

@@ -135,4 +135,5 @@ class Renderer:
         render_time_s = starter.elapsed_time(ender) / 1000.0
         print(f"Accelerated Render time: {render_time_s:.4f} seconds")
         return {"rgb_map_f": out["rgb_map_f"], "depth_map_f": out["depth_map_f"], "acc_map_f": out["acc_map_f"],
-                "render_time": render_time_s, "n_queried": out["n_queried"]}
+                "render_time": render_time_s, "n_queried": out["n_queried"], "n_evaluated": out["n_evaluated"],
+                "rounds": out["rounds"]}

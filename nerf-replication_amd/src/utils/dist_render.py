@@ -51,7 +51,7 @@ def render_distributed(renderer, batch, accelerated: bool = False, keys=None):
         elif isinstance(v, (int, float)):
             dev = flat.device if flat.device.type != "cpu" or dist.get_backend() == "gloo" else "cuda"
             t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.SUM if k == "n_queried" else dist.ReduceOp.MAX)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM if k in ("n_queried", "n_evaluated") else dist.ReduceOp.MAX)
             res[k] = type(v)(t.item())
         else:
             res[k] = v
