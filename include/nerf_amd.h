@@ -112,6 +112,12 @@ int nerf_mlp_bwd(const void* packed_bwd, int dtype, const float* d_raw, int64_t 
 int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64_t M, const uint16_t* masks, void* dz,
                     hipStream_t stream);
 int nerf_mlp_bwd_dw(int dtype, int64_t M, const void* act, const void* dz, float* grad, hipStream_t stream);
+/* dW/db with a workspace of nerf_mlp_dw_workspace_bytes(dtype, M): each work item writes its partial
+ * sums to its own slice and a second kernel adds them per parameter in a fixed order, so the gradient
+ * is bit-reproducible run to run (workspace == NULL: fp32 atomics, as nerf_mlp_bwd_dw). */
+int64_t nerf_mlp_dw_workspace_bytes(int dtype, int64_t M);
+int nerf_mlp_bwd_dw_ws(int dtype, int64_t M, const void* act, const void* dz, float* grad, void* workspace,
+                       hipStream_t stream);
 
 /* ---- (a14) evaluator metrics (src/evaluators/nerf.py:23-45) --------------------------------------
  * pred / gt fp32 [H,W,3] on the device -> out (device, 4 doubles): PSNR of the float images,

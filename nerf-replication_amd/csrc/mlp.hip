@@ -1046,7 +1046,16 @@ struct DwArgs {
   float* grad;        // flat [NET_PARAMS], accumulated
   int item_off[NDWJOB + 1];
   int job_of[NDWJOB];
+  float* partial;     // per-item partial sums (deterministic mode, dw_reduce_kernel) or null (atomics)
 };
+
+// Deterministic mode: every work item writes its accumulators, fragment-native, to its own
+// slice of `partial` -- per wave DW_PSLOTS tiles (acc[0..9] -> 0..9, acc2 -> 10) of 64 lanes x
+// 16 floats, then 128 floats of row sums (dbias lanes 0..63, dbias2 lanes 0..63) -- and
+// dw_reduce_kernel adds the items of each job in item order: the same sum on every run.
+constexpr int DW_PSLOTS = 11;
+constexpr int DW_PWAVE = DW_PSLOTS * 1024 + 128;   // floats per wave
+constexpr int DW_PITEM = DW_WAVES * DW_PWAVE;      // floats per item
 
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n in [0, 63] (n is a multiple of G here)
 __device__ __forceinline__ void wait_vmcnt_rt(int n) {
@@ -1329,6 +1338,24 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
     buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
 
+  if (a.partial) {  // deterministic: the item's sums to its own slice (dw_reduce_kernel adds them)
+    float* pw = a.partial + ((int64_t)blockIdx.x * DW_WAVES + wave) * DW_PWAVE;
+    auto put = [&](int slot, const f32x16& v) {
+      float* d = pw + slot * 1024 + lane * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *(float4*)(d + q * 256) = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    };
+    constexpr int NACC = JD.kind == DW_VR ? 9 : JD.kt;
+    if (!vr_rgb) {
+      sfor<NACC>([&](auto tt) { put(decltype(tt)::value, acc[decltype(tt)::value]); });
+    } else {
+      put(0, acc[0]);
+    }
+    if constexpr (JD.kind == DW_FA) put(10, acc2);
+    pw[DW_PSLOTS * 1024 + lane] = dbias;
+    pw[DW_PSLOTS * 1024 + 64 + lane] = dbias2;
+    return;
+  }
   // flush (state_dict layout: weight [N][K] row-major)
   if constexpr (JD.kind == DW_REG) {
     constexpr int WP = gemm_weight(J);
@@ -1378,6 +1405,97 @@ __global__ void __launch_bounds__(DW_WAVES * 64) dw_kernel(DwArgs a) {
     case 7: dw_job<P, 7>(a, b_begin, b_end, lds); break;
     case 8: dw_job<P, 8>(a, b_begin, b_end, lds); break;
     default: dw_job<P, 9>(a, b_begin, b_end, lds); break;
+  }
+}
+
+// flat-gradient index of element (wave w, slot t, lane, register rho) of job J's partial
+// accumulators, or -1 (padding / unused): the inverse of the dw_flush / dw_flush_bias maps.
+// Slot DW_PSLOTS holds the row sums: q = element (0..127) -- q < 32: dbias of lanes q and
+// q + 32 (returned for q only; the caller adds both), 64 <= q < 96: dbias2 likewise.
+template <int J>
+__device__ __forceinline__ int64_t dw_param_index(int w, int t, int lane, int rho) {
+  constexpr DwJobDesc JD = dw_job_desc(J);
+  const int h = lane >> 5, colf = perm_row(lane & 31), nrow = perm_row(acc_row(rho, h));
+  if constexpr (JD.kind == DW_REG) {
+    constexpr int WP = gemm_weight(J);
+    if (t >= JD.kt) return -1;
+    const int c0 = gemm_col0(J, t), cv = gemm_col_valid(J, t);
+    if (colf >= cv) return -1;
+    return param_offset(WP) + (int64_t)(32 * w + nrow) * weight_K(WP) + c0 + colf;
+  } else if constexpr (JD.kind == DW_FA) {
+    if (t < 8) return param_offset(P_FW) + (int64_t)(32 * w + nrow) * 256 + 32 * t + colf;
+    if (t == 10 && nrow < 1) return param_offset(P_AW) + 32 * w + colf;
+    return -1;
+  } else {
+    if (w < 4) {
+      if (t >= 9 || colf >= (t < 8 ? 32 : 27)) return -1;
+      return param_offset(P_VW) + (int64_t)(32 * w + nrow) * 283 + 32 * t + colf;
+    }
+    if (t == 0 && nrow < 3) return param_offset(P_RW) + (int64_t)nrow * 128 + 32 * (w - 4) + colf;
+    return -1;
+  }
+}
+template <int J>
+__device__ __forceinline__ int64_t dw_bias_index(int w, int q) {
+  constexpr DwJobDesc JD = dw_job_desc(J);
+  const int n = perm_row(q & 31);
+  if (q < 32) {
+    if constexpr (JD.kind == DW_REG) return param_offset(gemm_weight(J) + 1) + 32 * w + n;
+    else if constexpr (JD.kind == DW_FA) return param_offset(P_FB) + 32 * w + n;
+    else {
+      if (w < 4) return param_offset(P_VB) + 32 * w + n;
+      return (w == 4 && n < 3) ? param_offset(P_RB) + n : -1;
+    }
+  }
+  if (q >= 64 && q < 96 && JD.kind == DW_FA && w == 0 && n < 1) return param_offset(P_AB);
+  return -1;
+}
+
+struct DwReduceArgs {
+  const float* partial;
+  float* grad;
+  int item_off[NDWJOB + 1];
+  int job_of[NDWJOB];
+};
+
+// one thread per (segment, wave, partial element); sums the segment's items in order
+template <int J>
+__device__ __forceinline__ void dw_reduce_job(const DwReduceArgs& a, int i0, int n, int w, int e) {
+  int64_t idx;
+  bool bias = e >= DW_PSLOTS * 1024;
+  if (!bias) {
+    const int t = e >> 10, r = e & 1023, q = r >> 8, lane = (r >> 2) & 63, rho = 4 * q + (r & 3);
+    idx = dw_param_index<J>(w, t, lane, rho);
+  } else {
+    idx = dw_bias_index<J>(w, e - DW_PSLOTS * 1024);
+  }
+  if (idx < 0) return;
+  const float* p = a.partial + ((int64_t)i0 * DW_WAVES + w) * DW_PWAVE + e;
+  float sum = 0.f;
+  for (int i = 0; i < n; ++i) {
+    const float* pi = p + (int64_t)i * DW_PITEM;
+    sum += bias ? pi[0] + pi[32] : pi[0];  // row sums: lanes q and q + 32 of one item
+  }
+  a.grad[idx] += sum;
+}
+
+__global__ void dw_reduce_kernel(DwReduceArgs a) {
+  const int seg = blockIdx.y;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (int64_t)DW_WAVES * DW_PWAVE) return;
+  const int w = (int)(g / DW_PWAVE), e = (int)(g % DW_PWAVE);
+  const int i0 = a.item_off[seg], n = a.item_off[seg + 1] - i0;
+  switch (a.job_of[seg]) {
+    case 0: dw_reduce_job<0>(a, i0, n, w, e); break;
+    case 1: dw_reduce_job<1>(a, i0, n, w, e); break;
+    case 2: dw_reduce_job<2>(a, i0, n, w, e); break;
+    case 3: dw_reduce_job<3>(a, i0, n, w, e); break;
+    case 4: dw_reduce_job<4>(a, i0, n, w, e); break;
+    case 5: dw_reduce_job<5>(a, i0, n, w, e); break;
+    case 6: dw_reduce_job<6>(a, i0, n, w, e); break;
+    case 7: dw_reduce_job<7>(a, i0, n, w, e); break;
+    case 8: dw_reduce_job<8>(a, i0, n, w, e); break;
+    default: dw_reduce_job<9>(a, i0, n, w, e); break;
   }
 }
 
@@ -1579,14 +1697,21 @@ int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64
   return check_launch("nerf_mlp_bwd_dx");
 }
 
-// dW/db only: grad += dz . act^T (grad must be zeroed or hold a running sum)
-int nerf_mlp_bwd_dw(int dtype, int64_t M, const void* act, const void* dz, float* grad, hipStream_t stream) {
+int64_t nerf_mlp_dw_workspace_bytes(int dtype, int64_t M) {
+  return nerf_mlp_dw_items(dtype, M) * (int64_t)DW_PITEM * 4;
+}
+
+// dW/db only: grad += dz . act^T (grad must be zeroed or hold a running sum).  workspace (nullable,
+// nerf_mlp_dw_workspace_bytes): per-item partial sums reduced in a fixed order -- bit-reproducible;
+// null: fp32 atomics.
+int nerf_mlp_bwd_dw_ws(int dtype, int64_t M, const void* act, const void* dz, float* grad, void* workspace,
+                       hipStream_t stream) {
   NERF_REQUIRE(dtype == 0 || dtype == 1, "nerf_mlp_bwd_dw: bad dtype %d", dtype);
   NERF_REQUIRE(M >= 0, "nerf_mlp_bwd_dw: M < 0");
   if (M == 0) return 0;
   NERF_REQUIRE(act && dz && grad, "nerf_mlp_bwd_dw: null pointer");
   const int64_t nblk = nerf_mlp_padded_samples(M) / 32;
-  DwArgs w{dz, act, nblk, grad, {}};
+  DwArgs w{dz, act, nblk, grad, {}, {}, (float*)workspace};
   dw_items(dtype, nblk, w.item_off, w.job_of);
   dim3 grid((unsigned)w.item_off[NDWJOB]);
   if (dtype == 0) {
@@ -1596,7 +1721,19 @@ int nerf_mlp_bwd_dw(int dtype, int64_t M, const void* act, const void* dz, float
     allow_lds(dw_kernel<PBF16>, dw_lds_bytes<PBF16>());
     hipLaunchKernelGGL((dw_kernel<PBF16>), grid, dim3(DW_WAVES * 64), dw_lds_bytes<PBF16>(), stream, w);
   }
-  return check_launch("nerf_mlp_bwd_dw");
+  if (int e = check_launch("nerf_mlp_bwd_dw")) return e;
+  if (workspace) {
+    DwReduceArgs r{(const float*)workspace, grad, {}, {}};
+    for (int k = 0; k <= NDWJOB; ++k) r.item_off[k] = w.item_off[k];
+    for (int k = 0; k < NDWJOB; ++k) r.job_of[k] = w.job_of[k];
+    const int64_t per = (int64_t)DW_WAVES * DW_PWAVE;
+    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((per + 255) / 256), NDWJOB), dim3(256), 0, stream, r);
+    return check_launch("nerf_mlp_bwd_dw_reduce");
+  }
+  return 0;
+}
+int nerf_mlp_bwd_dw(int dtype, int64_t M, const void* act, const void* dz, float* grad, hipStream_t stream) {
+  return nerf_mlp_bwd_dw_ws(dtype, M, act, dz, grad, nullptr, stream);
 }
 
 int nerf_mlp_bwd(const void* packed_bwd, int dtype, const float* d_raw, int64_t M, const void* act,

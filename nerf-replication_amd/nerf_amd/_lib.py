@@ -45,6 +45,8 @@ SIGNATURES = {
     "nerf_mlp_bwd": (_i32, [_p, _i32, _p, _i64, _p, _p, _p, _p, _p]),
     "nerf_mlp_bwd_dx": (_i32, [_p, _i32, _p, _i64, _p, _p, _p]),
     "nerf_mlp_bwd_dw": (_i32, [_i32, _i64, _p, _p, _p, _p]),
+    "nerf_mlp_dw_workspace_bytes": (_i64, [_i32, _i64]),
+    "nerf_mlp_bwd_dw_ws": (_i32, [_i32, _i64, _p, _p, _p, _p, _p]),
     "nerf_grid_index": (_i32, [_p, _i64, _p, _i32, _p, _p, _p, _p]),
     "nerf_bake_num_points": (_i64, [_i32, _i32]),
     "nerf_bake_points": (_i32, [_i32, _p, _i32, _p, _p]),

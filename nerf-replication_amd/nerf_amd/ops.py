@@ -310,6 +310,8 @@ NET_PARAM_NAMES = (
 
 _PARAM_GENERATION = [0]
 _DIRECT_GRAD = [0]
+# dW partial sums reduced in a fixed order (bit-reproducible gradients) instead of fp32 atomics
+DETERMINISTIC_DW = True
 
 
 class direct_grad:
@@ -458,8 +460,11 @@ class _MLP(torch.autograd.Function):
         with kernel_timer("mlp_bwd_dx", ctx.M):
             check(lib().nerf_mlp_bwd_dx(ptr(ctx.packed_bwd), ctx.dtype, ptr(g_raw), ctx.M, ptr(ctx.masks), ptr(dz), s),
                   "nerf_mlp_bwd_dx")
+        ws = torch.empty(lib().nerf_mlp_dw_workspace_bytes(ctx.dtype, ctx.M), dtype=torch.uint8, device=dev) \
+            if DETERMINISTIC_DW else None
         with kernel_timer("mlp_bwd_dw", ctx.M):
-            check(lib().nerf_mlp_bwd_dw(ctx.dtype, ctx.M, ptr(ctx.act), ptr(dz), ptr(grad), s), "nerf_mlp_bwd_dw")
+            check(lib().nerf_mlp_bwd_dw_ws(ctx.dtype, ctx.M, ptr(ctx.act), ptr(dz), ptr(grad), ptr(ws), s),
+                  "nerf_mlp_bwd_dw")
         ctx.act = ctx.masks = None
         # the net's data-parallel bucket starts after its last pending chunk's dW only
         ctx.packer.backward_done(grad if direct is not None else None)

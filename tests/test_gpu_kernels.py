@@ -346,3 +346,36 @@ def test_image_metrics_match_host_evaluator(cuda, ops, H, W, noise):
     ref_ssim = ssim_metric_uint8((p_np * 255).astype(np.uint8), (g_np * 255).astype(np.uint8))
     assert abs(psnr - ref_psnr) < 1e-4, (psnr, ref_psnr)
     assert abs(ssim - ref_ssim) < 1e-9, (ssim, ref_ssim)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_mlp_dw_deterministic(cuda, ops, seeded_state, dtype):
+    """dW with the workspace (per-item partials, fixed-order reduce) is bit-identical run to
+    run and equal, to fp32 summation-order rounding, to the atomic accumulation."""
+    from nerf_amd._lib import check, lib, ptr, stream_of
+    g = torch.Generator().manual_seed(21)
+    M = 70001
+    code = ops.dtype_code(dtype)
+    params = [seeded_state[f"model.{n}"].to(cuda).contiguous() for n in ops.NET_PARAM_NAMES]
+    packer = ops.PackedMLP(params)
+    pts = (torch.rand(M, 3, generator=g) * 3 - 1.5).to(cuda)
+    vd = torch.nn.functional.normalize(torch.randn(M // 7 + 1, 3, generator=g), dim=-1).to(cuda)
+    L = lib()
+    act = torch.empty(L.nerf_mlp_act_bytes(code, M), dtype=torch.uint8, device=cuda)
+    masks = torch.empty(L.nerf_mlp_mask_bytes(M), dtype=torch.uint8, device=cuda)
+    dz = torch.empty(L.nerf_mlp_dz_bytes(code, M), dtype=torch.uint8, device=cuda)
+    raw = torch.empty(M, 4, device=cuda)
+    s = stream_of(pts)
+    check(L.nerf_mlp_fwd(ptr(packer.get(code, 0)), code, ptr(pts), ptr(vd), 7, None, M, 1, ptr(raw), ptr(act),
+                         ptr(masks), s), "fwd")
+    d_raw = torch.randn(M, 4, generator=g).to(cuda)
+    check(L.nerf_mlp_bwd_dx(ptr(packer.get(code, 1)), code, ptr(d_raw), M, ptr(masks), ptr(dz), s), "dx")
+    ws = torch.empty(L.nerf_mlp_dw_workspace_bytes(code, M), dtype=torch.uint8, device=cuda)
+    outs = []
+    for use_ws in (True, True, False):
+        grad = torch.zeros(L.nerf_mlp_net_params(), device=cuda)
+        check(L.nerf_mlp_bwd_dw_ws(code, M, ptr(act), ptr(dz), ptr(grad), ptr(ws) if use_ws else None, s), "dw")
+        outs.append(grad.cpu())
+    assert torch.equal(outs[0], outs[1])
+    scale = float(outs[2].abs().max())
+    assert float((outs[0] - outs[2]).abs().max()) <= 1e-5 * scale
