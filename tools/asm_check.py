@@ -20,17 +20,32 @@ KERNELS = ["fwd_kernel<nerf::mlp::PBF16, true, false>", "fwd_kernel<nerf::mlp::P
 
 
 def build_asm(tmp, kernels=None):
+    """gfx950 assembly of the given kernel instantiations, one hipcc process per kernel (in
+    parallel), concatenated."""
     kernels = kernels or KERNELS
-    src = os.path.join(tmp, "k.hip")
     args = {"fwd": "(nerf::mlp::FwdArgs)", "dx_": "(nerf::mlp::DxArgs)", "dw_": "(nerf::mlp::DwArgs)"}
-    with open(src, "w") as f:
-        f.write("#define NERF_MLP_DEVICE_ONLY\n")
-        f.write(f'#include "{ROOT}/nerf-replication_amd/csrc/mlp.hip"\n')
-        for k in kernels:
+    procs = []
+    for i, k in enumerate(kernels):
+        src = os.path.join(tmp, f"k{i}.hip")
+        with open(src, "w") as f:
+            f.write("#define NERF_MLP_DEVICE_ONLY\n")
+            f.write(f'#include "{ROOT}/nerf-replication_amd/csrc/mlp.hip"\n')
             f.write(f"template __global__ void nerf::mlp::{k}{args[k[:3]]};\n")
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include",
-                    "--cuda-device-only", "-S", src, "-o", os.path.join(tmp, "k.s")], check=True, cwd=tmp)
-    return open(os.path.join(tmp, "k.s")).read()
+        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                                       f"-I{ROOT}/include", "--cuda-device-only", "-S", src, "-o",
+                                       os.path.join(tmp, f"k{i}.s")], cwd=tmp, stdout=subprocess.DEVNULL,
+                                      stderr=subprocess.DEVNULL))
+    for p in procs:
+        if p.wait() != 0:
+            raise RuntimeError("hipcc failed")
+    asm = []
+    for i, k in enumerate(kernels):
+        text = open(os.path.join(tmp, f"k{i}.s")).read()
+        # keep the instantiated kernel only (every file also carries the non-template reduce kernel)
+        if "dw_reduce_kernel" not in k:
+            text = re.sub(r"^_ZN4nerf3mlp16dw_reduce_kernel\w*:.*?s_endpgm", "", text, flags=re.S | re.M)
+        asm.append(text)
+    return "\n".join(asm)
 
 
 def check(asm):
@@ -53,7 +68,7 @@ def check(asm):
             if m and i + 1 < len(lines) and "s_barrier" in lines[i + 1] and since is not None:
                 waits += 1
                 unsafe += int(m.group(1)) > since
-        straight = "dw_kernel" in name or not loops
+        straight = "dw_kernel" in name or "dw_reduce" in name or not loops
         ok = straight and not unsafe
         bad += not ok
         print(f"{'ok ' if ok else 'BAD'} {name[:70]:70s} loops={len(loops)} counted_waits={waits} unsafe={unsafe}")
