@@ -85,12 +85,20 @@ def pmc_traffic(kernel, dtype):
 
 
 def setup_dist():
+    """One process per GPU over RCCL ("nccl").  NERF_BENCH_BACKEND=gloo (rehearsal only) lets
+    several ranks share the GPUs of a smaller box (device = local rank mod device count)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("NERF_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend, init_method="env://")
     return world, rank, torch.device("cuda", local)
 
 
