@@ -31,7 +31,10 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 // ------------------------------------------------------------------------------------
 // precision policies
 // ------------------------------------------------------------------------------------
+enum PKind { K_F32 = 0, K_BF16 = 1, K_BF16X3 = 2 };
+
 struct PF32 {
+  static constexpr int KIND = K_F32;
   static constexpr int CH = 4;     // 1 KiB chunks per 32-feature input tile
   static constexpr int E = 4;      // elements per lane per chunk
   static constexpr int WAVES = 4;  // one wave per SIMD (<= 512 VGPR+AGPR)
@@ -50,6 +53,9 @@ struct PF32 {
   static __device__ __forceinline__ void set(Tile& t, int rho, float x) { t.v[rho] = x; }
   static __device__ __forceinline__ float get(const Tile& t, int rho) { return t.v[rho]; }
   static __device__ __forceinline__ Store cvt(float x) { return x; }
+  // packed weight element e of chunk c: accumulator register (k order) and stored value
+  static __host__ __device__ constexpr int rho_of(int c, int e) { return c * E + e; }
+  static __device__ __forceinline__ Store cvt_c(float x, int) { return x; }
   static __device__ __forceinline__ f32x16 mma_k(uint4 a, uint4 b, f32x16 acc) {
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
@@ -67,6 +73,7 @@ struct PF32 {
 };
 
 struct PBF16 {
+  static constexpr int KIND = K_BF16;
   static constexpr int CH = 2;
   static constexpr int E = 8;
   static constexpr int WAVES = 8;  // two waves per SIMD (<= 256 VGPR)
@@ -81,6 +88,8 @@ struct PBF16 {
   static __device__ __forceinline__ void set(Tile& t, int rho, float x) { t.b[rho >> 3][rho & 7] = (__bf16)x; }
   static __device__ __forceinline__ float get(const Tile& t, int rho) { return (float)t.b[rho >> 3][rho & 7]; }
   static __device__ __forceinline__ Store cvt(float x) { return (__bf16)x; }
+  static __host__ __device__ constexpr int rho_of(int c, int e) { return c * E + e; }
+  static __device__ __forceinline__ Store cvt_c(float x, int) { return (__bf16)x; }
   static __device__ __forceinline__ f32x16 mma_k(uint4 a, uint4 b, f32x16 acc) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                    __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
@@ -93,6 +102,48 @@ struct PBF16 {
     return s;
   }
   static __device__ __forceinline__ uint4 chunk(const Tile& t, int c) { return __builtin_bit_cast(uint4, t.b[c]); }
+};
+
+// bf16x3: every fp32 operand x is split x = hi + lo (hi = bf16(x), lo = bf16(x - hi), 16
+// significant bits together) and a product is hi*hi + hi*lo + lo*hi on the bf16 MFMA with fp32
+// accumulation -- 3 bf16 MFMAs (96 cycles) per K = 16 step instead of 8 fp32 ones (512 cycles),
+// at ~1e-5 relative error per dot product (fp32-class; the fp32 parity tests hold at 1e-4).
+// Weights: chunks 0, 1 = hi of k 0-7 / 8-15, chunks 2, 3 = lo.  Tiles hold hi and lo (16
+// VGPRs, as fp32), stored as 4 KiB tile-blocks (hi 2 KiB then lo 2 KiB).
+struct PBF3 {
+  static constexpr int KIND = K_BF16X3;
+  static constexpr int CH = 4;
+  static constexpr int E = 8;
+  static constexpr int WAVES = 4;  // one wave per SIMD (16-VGPR tiles)
+  static constexpr int ESIZE = 4;
+  static constexpr int SPL = 8;
+  static constexpr bool FAST_PE = false;  // fp32-accurate PE (libm sincosf), then split
+  using Store = __bf16;
+  struct Tile { bf16x8 hi[2], lo[2]; };
+  static __device__ __forceinline__ f32x16 mma(uint4 a, const Tile& b, int c, f32x16 acc) {
+    const bf16x8 av = __builtin_bit_cast(bf16x8, a);
+    if (c < 2) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, b.hi[c], acc, 0, 0, 0);
+      return __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, b.lo[c], acc, 0, 0, 0);
+    }
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, b.hi[c - 2], acc, 0, 0, 0);
+  }
+  static __device__ __forceinline__ void set(Tile& t, int rho, float x) {
+    const __bf16 h = (__bf16)x;
+    t.hi[rho >> 3][rho & 7] = h;
+    t.lo[rho >> 3][rho & 7] = (__bf16)(x - (float)h);
+  }
+  static __device__ __forceinline__ float get(const Tile& t, int rho) {
+    return (float)t.hi[rho >> 3][rho & 7] + (float)t.lo[rho >> 3][rho & 7];
+  }
+  static __host__ __device__ constexpr int rho_of(int c, int e) { return (c & 1) * E + e; }
+  static __device__ __forceinline__ Store cvt_c(float x, int c) {
+    const __bf16 h = (__bf16)x;
+    return c < 2 ? h : (__bf16)(x - (float)h);
+  }
+  static __device__ __forceinline__ uint4 chunk(const Tile& t, int c) {
+    return __builtin_bit_cast(uint4, c < 2 ? t.hi[c] : t.lo[c - 2]);
+  }
 };
 
 // ReLU-mask bit of accumulator register rho of a tile: the tile's 16 bits sit at positions
@@ -180,7 +231,7 @@ __global__ void pack_kernel(ParamPtrs prm, UnitOffsets uo, char* out) {
   typename P::Store vals[P::E];
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
-    const int rho = c * P::E + e;
+    const int rho = P::rho_of(c, e);
     const int ar = acc_row(rho, h);
     float v = 0.f;
     if (DIR == 0) {
@@ -195,7 +246,7 @@ __global__ void pack_kernel(ParamPtrs prm, UnitOffsets uo, char* out) {
       const int row = fwd_out_row0(L, t) + ar, col = bwd_out_colbase(s, j) + r;
       if (ar < fwd_out_valid(L, t)) v = prm.p[wp][(int64_t)row * weight_K(wp) + col];
     }
-    vals[e] = P::cvt(v);
+    vals[e] = P::cvt_c(v, c);
   }
 #pragma unroll
   for (int e = 0; e < P::E; ++e) ((typename P::Store*)dst)[e] = vals[e];
@@ -380,7 +431,9 @@ __host__ __device__ constexpr Step group_step(int g, int k) {
 #ifndef NERF_FINISH_DELAY
 #define NERF_FINISH_DELAY 3
 #endif
-template <class P> __host__ __device__ constexpr int prefetch_depth() { return P::CH == 2 ? NERF_PREFETCH_BF16 : 2; }
+template <class P> __host__ __device__ constexpr int prefetch_depth() {
+  return P::KIND == K_F32 ? 2 : NERF_PREFETCH_BF16;  // a bf16 / bf16x3 step is 1-2 short MFMAs
+}
 constexpr int FINISH_DELAY = NERF_FINISH_DELAY;
 
 // W: the wave object; it provides in_tile<u, t>(), prefetch<u>() (issue unit u's side
@@ -643,7 +696,7 @@ struct FwdWave {
     if constexpr (L <= L7 || L == LV) {
       Tile out;
       uint32_t bits = 0;  // mask bits of this tile (mask_bit layout)
-      if constexpr (P::CH == 2) {
+      if constexpr (P::KIND == K_BF16) {
         // bf16: pack pairs first, then ReLU and mask on the packed pairs (2 values per VALU)
         uint32_t d[8];
 #pragma unroll
@@ -682,7 +735,7 @@ struct FwdWave {
     } else if constexpr (L == LFA) {
       if constexpr (n < 8) {  // feature_linear: no activation
         Tile out;
-        if constexpr (P::CH == 2) {
+        if constexpr (P::KIND == K_BF16) {
           uint32_t d[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k) d[k] = pack_bf16(acc[2 * k], acc[2 * k + 1]);
@@ -903,7 +956,7 @@ struct DxWave {
       w >>= 8 * (j & 1);
     }
     Tile out;
-    if constexpr (P::CH == 2) {
+    if constexpr (P::KIND == K_BF16) {
       uint32_t d[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -1034,7 +1087,7 @@ __host__ __device__ constexpr int dw_job_tiles(int j) { return dw_job_desc(j).nd
 #ifndef NERF_DW_NBUF_BF16
 #define NERF_DW_NBUF_BF16 4
 #endif
-template <class P> __host__ __device__ constexpr int dw_nbuf() { return P::CH == 2 ? NERF_DW_NBUF_BF16 : 2; }
+template <class P> __host__ __device__ constexpr int dw_nbuf() { return P::KIND == K_BF16 ? NERF_DW_NBUF_BF16 : 2; }
 __host__ __device__ constexpr int perm_row(int i) { return acc_row(i & 15, i >> 4); }
 
 // work items: segment s = items [item_off[s], item_off[s + 1]) of job job_of[s]
@@ -1141,18 +1194,32 @@ __device__ __forceinline__ float dw_frag_f32(const char* tile, int s, int lane) 
 // one K step (16 samples bf16 / 2 samples fp32) of C += A B^T for A = LDS tile `at`
 template <class P>
 __device__ __forceinline__ f32x16 dw_mma(const char* at, const char* bt, int s, int lane, f32x16 acc) {
-  if constexpr (P::CH == 2)
+  if constexpr (P::KIND == K_BF16) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(dw_frag_bf16(at, s, lane), dw_frag_bf16(bt, s, lane), acc, 0, 0, 0);
-  else
+  } else if constexpr (P::KIND == K_BF16X3) {  // tile-block = hi (2 KiB) then lo (2 KiB)
+    const bf16x8 ah = dw_frag_bf16(at, s, lane), al = dw_frag_bf16(at + 2048, s, lane);
+    const bf16x8 bh = dw_frag_bf16(bt, s, lane), bl = dw_frag_bf16(bt + 2048, s, lane);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  } else {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(dw_frag_f32(at, s, lane), dw_frag_f32(bt, s, lane), acc, 0, 0, 0);
+  }
 }
 template <class P>
 __device__ __forceinline__ float dw_rowsum(const char* at, int s, int lane) {
-  if constexpr (P::CH == 2) {
+  if constexpr (P::KIND != K_F32) {
     const bf16x8 v = dw_frag_bf16(at, s, lane);
     float r = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) r += (float)v[e];
+    if constexpr (P::KIND == K_BF16X3) {
+      const bf16x8 l = dw_frag_bf16(at + 2048, s, lane);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q += (float)l[e];
+      r += q;
+    }
     return r;
   } else {
     return dw_frag_f32(at, s, lane);
@@ -1212,7 +1279,7 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
   constexpr int NCHUNK = NT * P::CH;
   constexpr int G = (NCHUNK + DW_WAVES - 1) / DW_WAVES;  // DMA per wave per block (uniform)
   constexpr int NBUF = dw_nbuf<P>(), D = NBUF - 1;
-  constexpr int KS = P::CH == 2 ? 2 : 16;    // K steps per 32-sample block
+  constexpr int KS = P::KIND == K_F32 ? 16 : 2;  // K steps per 32-sample block
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;  // (kept divergent to the compiler: uniform branching spills)
 
@@ -1232,7 +1299,8 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
     for (int t = 0; t < NT; ++t)
       if (t == q) tau = t < JD.nd ? JD.dz[t] : JD.act[t - JD.nd];
     const int ntiles = is_dz ? ZT_TILES : AT_TILES;
-    const int piece = P::CH == 2 ? dw_unswz(c, lane) : NERF_DW_SWZ_F32 ? dw_unswz_f32(c, lane) : lane;  // swizzled
+    // swizzled rings (bf16x3: chunks 2, 3 are the lo tile, swizzled as chunks 0, 1)
+    const int piece = P::KIND != K_F32 ? dw_unswz(c & 1, lane) : NERF_DW_SWZ_F32 ? dw_unswz_f32(c, lane) : lane;
     sb[i] = uniform_ptr((const char*)(is_dz ? a.dz : a.act) + tile_kib(a.nblk, ntiles, tau, 0, c, P::CH) * 1024);
     voff[i] = (uint32_t)(piece * 16);
     bstride[i] = block_stride_kib(ntiles, P::CH) * 1024;
@@ -1277,7 +1345,7 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
     __builtin_amdgcn_sched_barrier(0);
     if (b + D < b_end) fetch(b + D, buf == 0 ? NBUF - 1 : buf - 1);
     const char* tiles = lds + buf * BUF;
-    if constexpr (P::CH == 4) {
+    if constexpr (P::KIND == K_F32) {
       // 16 K steps as 4 rounds of 4 (s = 4 a + b): the rounds are a real loop (the bases step
       // by 128 B), so the scheduler's window -- and the fragments it keeps in flight -- is
       // one round, not the whole block
@@ -1479,6 +1547,7 @@ __device__ __forceinline__ void dw_reduce_job(const DwReduceArgs& a, int i0, int
   a.grad[idx] += sum;
 }
 
+#if !defined(NERF_MLP_PREC)  // non-template: defined in the C-ABI translation unit only
 __global__ void dw_reduce_kernel(DwReduceArgs a) {
   const int seg = blockIdx.y;
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1498,6 +1567,7 @@ __global__ void dw_reduce_kernel(DwReduceArgs a) {
     default: dw_reduce_job<9>(a, i0, n, w, e); break;
   }
 }
+#endif
 
 }  // namespace mlp
 }  // namespace nerf
@@ -1542,46 +1612,111 @@ static void launch_fwd_any(const FwdArgs& a, bool store, bool density, hipStream
   else launch_fwd<P, false, false>(a, stream);
 }
 
+// Every kernel launch of one precision, instantiated in that precision's translation unit
+// (mlp.hip compiled with -DNERF_MLP_PREC=0 fp32 / 1 bf16 / 2 bf16x3, csrc/Makefile); the C-ABI
+// unit (no NERF_MLP_PREC) only declares them, so the three precisions compile in parallel.
+namespace nerf {
+namespace mlp {
+template <class P>
+void mlp_pack_impl(const ParamPtrs& prm, int dir, char* dst, hipStream_t stream) {
+  const int64_t n = total_chunks(P::CH, dir) * 64;
+  dim3 grid((unsigned)((n + 255) / 256));
+  if (dir == 0) hipLaunchKernelGGL((pack_kernel<P, 0>), grid, dim3(256), 0, stream, prm, unit_offsets<P::CH, 0>(), dst);
+  else hipLaunchKernelGGL((pack_kernel<P, 1>), grid, dim3(256), 0, stream, prm, unit_offsets<P::CH, 1>(), dst);
+}
+template <class P>
+void mlp_fwd_train_impl(const FwdArgs& a, hipStream_t stream) {
+  launch_fwd<P, true, false>(a, stream);
+}
+template <class P>
+void mlp_fwd_infer_impl(const FwdArgs& a, bool density, hipStream_t stream) {
+  if (density) launch_fwd<P, false, true>(a, stream);
+  else launch_fwd<P, false, false>(a, stream);
+}
+template <class P>
+void mlp_dx_impl(const DxArgs& x, int64_t ldm, hipStream_t stream) {
+  launch_dx<P>(x, ldm, stream);
+}
+template <class P>
+void mlp_dw_impl(const DwArgs& w, dim3 grid, hipStream_t stream) {
+  allow_lds(dw_kernel<P>, dw_lds_bytes<P>());
+  hipLaunchKernelGGL((dw_kernel<P>), grid, dim3(DW_WAVES * 64), dw_lds_bytes<P>(), stream, w);
+}
+// explicit instantiations, split further by part (-DNERF_MLP_PART: 0 training forward, 1 inference
+// and density forwards, 2 dX + pack, 3 dW) so that no translation unit holds more than one or two
+// of the large straight-line kernels
+#define NERF_MLP_I_PACK(EXT, P) EXT template void mlp_pack_impl<P>(const ParamPtrs&, int, char*, hipStream_t);
+#define NERF_MLP_I_FWDT(EXT, P) EXT template void mlp_fwd_train_impl<P>(const FwdArgs&, hipStream_t);
+#define NERF_MLP_I_FWDI(EXT, P) EXT template void mlp_fwd_infer_impl<P>(const FwdArgs&, bool, hipStream_t);
+#define NERF_MLP_I_DX(EXT, P) EXT template void mlp_dx_impl<P>(const DxArgs&, int64_t, hipStream_t);
+#define NERF_MLP_I_DW(EXT, P) EXT template void mlp_dw_impl<P>(const DwArgs&, dim3, hipStream_t);
+#define NERF_MLP_IMPLS(EXT, P) \
+  NERF_MLP_I_PACK(EXT, P) NERF_MLP_I_FWDT(EXT, P) NERF_MLP_I_FWDI(EXT, P) NERF_MLP_I_DX(EXT, P) NERF_MLP_I_DW(EXT, P)
+#if !defined(NERF_MLP_PREC)
+NERF_MLP_IMPLS(extern, PF32)
+NERF_MLP_IMPLS(extern, PBF16)
+NERF_MLP_IMPLS(extern, PBF3)
+#else
+#if NERF_MLP_PREC == 0
+#define NERF_PP PF32
+#elif NERF_MLP_PREC == 1
+#define NERF_PP PBF16
+#else
+#define NERF_PP PBF3
+#endif
+#if !defined(NERF_MLP_PART) || NERF_MLP_PART == 0
+NERF_MLP_I_FWDT(, NERF_PP)
+#endif
+#if !defined(NERF_MLP_PART) || NERF_MLP_PART == 1
+NERF_MLP_I_FWDI(, NERF_PP)
+#endif
+#if !defined(NERF_MLP_PART) || NERF_MLP_PART == 2
+NERF_MLP_I_DX(, NERF_PP)
+NERF_MLP_I_PACK(, NERF_PP)
+#endif
+#if !defined(NERF_MLP_PART) || NERF_MLP_PART == 3
+NERF_MLP_I_DW(, NERF_PP)
+#endif
+#endif
+}  // namespace mlp
+}  // namespace nerf
+
+#if !defined(NERF_MLP_PREC)
+
 extern "C" {
 
 int64_t nerf_mlp_net_params(void) { return NET_PARAMS; }
 int64_t nerf_mlp_param_offset(int i) { return (i >= 0 && i <= NPARAM) ? param_offset(i) : -1; }
 
 int64_t nerf_mlp_packed_bytes(int dtype, int dir) {
-  if ((dtype != 0 && dtype != 1) || (dir != 0 && dir != 1)) return -1;
-  return total_chunks(dtype == 0 ? PF32::CH : PBF16::CH, dir) * 1024;
+  if (dtype < 0 || dtype > 2 || (dir != 0 && dir != 1)) return -1;
+  return total_chunks(dtype == 1 ? PBF16::CH : PF32::CH, dir) * 1024;  // bf16x3: CH 4 as fp32
 }
 
 int64_t nerf_mlp_padded_samples(int64_t M) { return (M + M_ALIGN - 1) / M_ALIGN * M_ALIGN; }
 int64_t nerf_mlp_act_bytes(int dtype, int64_t M) {
-  return (int64_t)A_ROWS * nerf_mlp_padded_samples(M) * (dtype == 0 ? 4 : 2);
+  return (int64_t)A_ROWS * nerf_mlp_padded_samples(M) * (dtype == 1 ? 2 : 4);
 }
 int64_t nerf_mlp_dz_bytes(int dtype, int64_t M) {
-  return (int64_t)Z_ROWS * nerf_mlp_padded_samples(M) * (dtype == 0 ? 4 : 2);
+  return (int64_t)Z_ROWS * nerf_mlp_padded_samples(M) * (dtype == 1 ? 2 : 4);
 }
 int64_t nerf_mlp_mask_bytes(int64_t M) { return nerf_mlp_padded_samples(M) / 32 * MASK_GROUPS * 64 * 16; }
 
 int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void* packed_bwd, hipStream_t stream) {
   NERF_REQUIRE(params != nullptr, "nerf_mlp_pack: params is null");
-  NERF_REQUIRE(dtype == 0 || dtype == 1, "nerf_mlp_pack: dtype must be 0 (f32) or 1 (bf16), got %d", dtype);
+  NERF_REQUIRE(dtype >= 0 && dtype <= 2, "nerf_mlp_pack: dtype must be 0 (f32), 1 (bf16) or 2 (bf16x3), got %d",
+               dtype);
   ParamPtrs prm;
   for (int i = 0; i < NPARAM; ++i) {
     NERF_REQUIRE(params[i] != nullptr, "nerf_mlp_pack: params[%d] is null", i);
     prm.p[i] = params[i];
   }
-  const int ch = dtype == 0 ? PF32::CH : PBF16::CH;
   for (int dir = 0; dir < 2; ++dir) {
     void* dst = dir == 0 ? packed_fwd : packed_bwd;
     if (!dst) continue;
-    const int64_t n = total_chunks(ch, dir) * 64;
-    dim3 grid((unsigned)((n + 255) / 256));
-    if (dtype == 0) {
-      if (dir == 0) hipLaunchKernelGGL((pack_kernel<PF32, 0>), grid, dim3(256), 0, stream, prm, unit_offsets<PF32::CH, 0>(), (char*)dst);
-      else hipLaunchKernelGGL((pack_kernel<PF32, 1>), grid, dim3(256), 0, stream, prm, unit_offsets<PF32::CH, 1>(), (char*)dst);
-    } else {
-      if (dir == 0) hipLaunchKernelGGL((pack_kernel<PBF16, 0>), grid, dim3(256), 0, stream, prm, unit_offsets<PBF16::CH, 0>(), (char*)dst);
-      else hipLaunchKernelGGL((pack_kernel<PBF16, 1>), grid, dim3(256), 0, stream, prm, unit_offsets<PBF16::CH, 1>(), (char*)dst);
-    }
+    if (dtype == 0) mlp_pack_impl<PF32>(prm, dir, (char*)dst, stream);
+    else if (dtype == 1) mlp_pack_impl<PBF16>(prm, dir, (char*)dst, stream);
+    else mlp_pack_impl<PBF3>(prm, dir, (char*)dst, stream);
     if (int e = check_launch("nerf_mlp_pack")) return e;
   }
   return 0;
@@ -1591,7 +1726,7 @@ int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void*
 int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const float* viewdirs, int samples_per_dir,
                  const int32_t* dir_index, int64_t M, int flags, float* raw, void* act, uint16_t* masks,
                  hipStream_t stream) {
-  NERF_REQUIRE(dtype == 0 || dtype == 1, "nerf_mlp_fwd: bad dtype %d", dtype);
+  NERF_REQUIRE(dtype >= 0 && dtype <= 2, "nerf_mlp_fwd: bad dtype %d", dtype);
   NERF_REQUIRE(M >= 0, "nerf_mlp_fwd: M < 0");
   if (M == 0) return 0;
   const bool store = flags & 1, density = flags & 2;
@@ -1602,8 +1737,15 @@ int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const floa
   NERF_REQUIRE(!(store && density), "nerf_mlp_fwd: store and density-only are exclusive");
   FwdArgs a{(const char*)packed_fwd, pts, viewdirs, dir_index, samples_per_dir, M,
             nerf_mlp_padded_samples(M) / 32, raw, act, masks};
-  if (dtype == 0) launch_fwd_any<PF32>(a, store, density, stream);
-  else launch_fwd_any<PBF16>(a, store, density, stream);
+  if (store) {
+    if (dtype == 0) mlp_fwd_train_impl<PF32>(a, stream);
+    else if (dtype == 1) mlp_fwd_train_impl<PBF16>(a, stream);
+    else mlp_fwd_train_impl<PBF3>(a, stream);
+  } else {
+    if (dtype == 0) mlp_fwd_infer_impl<PF32>(a, density, stream);
+    else if (dtype == 1) mlp_fwd_infer_impl<PBF16>(a, density, stream);
+    else mlp_fwd_infer_impl<PBF3>(a, density, stream);
+  }
   return check_launch("nerf_mlp_fwd");
 }
 
@@ -1686,14 +1828,15 @@ int64_t nerf_mlp_dw_items(int dtype, int64_t M) {
 // dX chain only: dz (per-layer output gradients, fragment-native tiles) from d_raw + masks
 int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64_t M, const uint16_t* masks, void* dz,
                     hipStream_t stream) {
-  NERF_REQUIRE(dtype == 0 || dtype == 1, "nerf_mlp_bwd_dx: bad dtype %d", dtype);
+  NERF_REQUIRE(dtype >= 0 && dtype <= 2, "nerf_mlp_bwd_dx: bad dtype %d", dtype);
   NERF_REQUIRE(M >= 0, "nerf_mlp_bwd_dx: M < 0");
   if (M == 0) return 0;
   NERF_REQUIRE(packed_bwd && d_raw && masks && dz, "nerf_mlp_bwd_dx: null pointer");
   const int64_t ldm = nerf_mlp_padded_samples(M);
   DxArgs x{(const char*)packed_bwd, d_raw, M, ldm / 32, masks, dz};
-  if (dtype == 0) launch_dx<PF32>(x, ldm, stream);
-  else launch_dx<PBF16>(x, ldm, stream);
+  if (dtype == 0) mlp_dx_impl<PF32>(x, ldm, stream);
+  else if (dtype == 1) mlp_dx_impl<PBF16>(x, ldm, stream);
+  else mlp_dx_impl<PBF3>(x, ldm, stream);
   return check_launch("nerf_mlp_bwd_dx");
 }
 
@@ -1706,7 +1849,7 @@ int64_t nerf_mlp_dw_workspace_bytes(int dtype, int64_t M) {
 // null: fp32 atomics.
 int nerf_mlp_bwd_dw_ws(int dtype, int64_t M, const void* act, const void* dz, float* grad, void* workspace,
                        hipStream_t stream) {
-  NERF_REQUIRE(dtype == 0 || dtype == 1, "nerf_mlp_bwd_dw: bad dtype %d", dtype);
+  NERF_REQUIRE(dtype >= 0 && dtype <= 2, "nerf_mlp_bwd_dw: bad dtype %d", dtype);
   NERF_REQUIRE(M >= 0, "nerf_mlp_bwd_dw: M < 0");
   if (M == 0) return 0;
   NERF_REQUIRE(act && dz && grad, "nerf_mlp_bwd_dw: null pointer");
@@ -1714,13 +1857,9 @@ int nerf_mlp_bwd_dw_ws(int dtype, int64_t M, const void* act, const void* dz, fl
   DwArgs w{dz, act, nblk, grad, {}, {}, (float*)workspace};
   dw_items(dtype, nblk, w.item_off, w.job_of);
   dim3 grid((unsigned)w.item_off[NDWJOB]);
-  if (dtype == 0) {
-    allow_lds(dw_kernel<PF32>, dw_lds_bytes<PF32>());
-    hipLaunchKernelGGL((dw_kernel<PF32>), grid, dim3(DW_WAVES * 64), dw_lds_bytes<PF32>(), stream, w);
-  } else {
-    allow_lds(dw_kernel<PBF16>, dw_lds_bytes<PBF16>());
-    hipLaunchKernelGGL((dw_kernel<PBF16>), grid, dim3(DW_WAVES * 64), dw_lds_bytes<PBF16>(), stream, w);
-  }
+  if (dtype == 0) mlp_dw_impl<PF32>(w, grid, stream);
+  else if (dtype == 1) mlp_dw_impl<PBF16>(w, grid, stream);
+  else mlp_dw_impl<PBF3>(w, grid, stream);
   if (int e = check_launch("nerf_mlp_bwd_dw")) return e;
   if (workspace) {
     DwReduceArgs r{(const float*)workspace, grad, {}, {}};
@@ -1743,4 +1882,5 @@ int nerf_mlp_bwd(const void* packed_bwd, int dtype, const float* d_raw, int64_t 
 }
 
 }  // extern "C"
+#endif  // !NERF_MLP_PREC
 #endif  // NERF_MLP_DEVICE_ONLY
