@@ -27,6 +27,13 @@ namespace mlp {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+
+// registers 2k, 2k+1 of an fp32 accumulator as one packed bf16 pair (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
+}
 
 // ------------------------------------------------------------------------------------
 // precision policies
@@ -51,6 +58,11 @@ struct PF32 {
     return acc;
   }
   static __device__ __forceinline__ void set(Tile& t, int rho, float x) { t.v[rho] = x; }
+  // a whole tile from its 16 register values
+  static __device__ __forceinline__ void pack16(Tile& t, const float (&v)[16]) {
+#pragma unroll
+    for (int rho = 0; rho < 16; ++rho) t.v[rho] = v[rho];
+  }
   static __device__ __forceinline__ float get(const Tile& t, int rho) { return t.v[rho]; }
   static __device__ __forceinline__ Store cvt(float x) { return x; }
   // packed weight element e of chunk c: accumulator register (k order) and stored value
@@ -86,6 +98,13 @@ struct PBF16 {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), b.b[c], acc, 0, 0, 0);
   }
   static __device__ __forceinline__ void set(Tile& t, int rho, float x) { t.b[rho >> 3][rho & 7] = (__bf16)x; }
+  static __device__ __forceinline__ void pack16(Tile& t, const float (&v)[16]) {
+    uint32_t d[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
+    t.b[0] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
+    t.b[1] = __builtin_bit_cast(bf16x8, make_uint4(d[4], d[5], d[6], d[7]));
+  }
   static __device__ __forceinline__ float get(const Tile& t, int rho) { return (float)t.b[rho >> 3][rho & 7]; }
   static __device__ __forceinline__ Store cvt(float x) { return (__bf16)x; }
   static __host__ __device__ constexpr int rho_of(int c, int e) { return c * E + e; }
@@ -133,6 +152,20 @@ struct PBF3 {
     t.hi[rho >> 3][rho & 7] = h;
     t.lo[rho >> 3][rho & 7] = (__bf16)(x - (float)h);
   }
+  // packed pairs: hi = v_cvt_pk_bf16_f32, its fp32 value by a shift / mask, lo = the
+  // residuals' pair (same values as set(), 4 VALU per pair instead of element inserts)
+  static __device__ __forceinline__ void pack16(Tile& t, const float (&v)[16]) {
+    uint32_t hw[8], lw[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      hw[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
+      lw[k] = pack_bf16(v[2 * k] - __uint_as_float(hw[k] << 16), v[2 * k + 1] - __uint_as_float(hw[k] & 0xffff0000u));
+    }
+    t.hi[0] = __builtin_bit_cast(bf16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
+    t.hi[1] = __builtin_bit_cast(bf16x8, make_uint4(hw[4], hw[5], hw[6], hw[7]));
+    t.lo[0] = __builtin_bit_cast(bf16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+    t.lo[1] = __builtin_bit_cast(bf16x8, make_uint4(lw[4], lw[5], lw[6], lw[7]));
+  }
   static __device__ __forceinline__ float get(const Tile& t, int rho) {
     return (float)t.hi[rho >> 3][rho & 7] + (float)t.lo[rho >> 3][rho & 7];
   }
@@ -154,15 +187,8 @@ __host__ __device__ constexpr int mask_bit(int rho) { return (rho >> 1) + 16 * (
 #define NERF_MASK_FROM_PACKED 0
 #endif
 
-typedef __attribute__((ext_vector_type(2))) float f32x2;
-typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 typedef __attribute__((ext_vector_type(2))) short i16x2;
 typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
-
-// registers 2k, 2k+1 of an fp32 accumulator as one packed bf16 pair (v_cvt_pk_bf16_f32)
-__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
-}
 // ReLU of a bf16 pair: sign-magnitude bf16 ordered as int16 -> v_pk_max_i16 with 0
 // (relu(bf16(x)) == bf16(relu(x)): rounding keeps the sign)
 __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t d) {
@@ -441,16 +467,25 @@ constexpr int FINISH_DELAY = NERF_FINISH_DELAY;
 #ifndef NERF_CROSS_GROUP_FINISH
 #define NERF_CROSS_GROUP_FINISH 1
 #endif
+// bf16x3 training forward: a finished accumulator carried over the barrier (plus the
+// hi / lo split of the finish) takes it past 512 VGPRs (139 spilled); finished in-group it
+// needs 438 and none
+#ifndef NERF_CROSS_GROUP_FINISH_BF3_FWD
+#define NERF_CROSS_GROUP_FINISH_BF3_FWD 0
+#endif
+template <class P, int DIR> __host__ __device__ constexpr bool cross_finish() {
+  return P::KIND == K_BF16X3 && DIR == 0 ? NERF_CROSS_GROUP_FINISH_BF3_FWD : NERF_CROSS_GROUP_FINISH;
+}
 // the unit finished inside group g: (first, last] = units whose finish is issued in g.
 // With CROSS_GROUP_FINISH the last unit of a group is finished FINISH_DELAY steps into the
 // next group (after the barrier), so no group ends in a VALU burst that every wave of the
 // workgroup runs at once; its stores then count against the next group's hand-off.
-template <int DIR, bool DENSITY, int CH>
+template <int DIR, bool DENSITY, int CH, bool CROSS>
 __host__ __device__ constexpr bool finished_in_group(int g, int u) {
   const auto& T = GroupTable<DIR, DENSITY, CH>::t;
   const Group G = T.g[g];
   const int last = G.u0 + G.n - 1;
-  if (!NERF_CROSS_GROUP_FINISH) return u >= G.u0 && u <= last;
+  if (!CROSS) return u >= G.u0 && u <= last;
   const bool prev = g > 0 && u == T.g[g - 1].u0 + T.g[g - 1].n - 1;
   return prev || (u >= G.u0 && (u < last || (u == last && g + 1 == T.n)));
 }
@@ -488,11 +523,11 @@ __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
     }
     acc = P::mma(a, w.template in_tile<S.u, S.t>(), S.c, acc);
     constexpr int U_BEFORE = S.j > 0 ? S.u - 1 : PREV_U;
-    if constexpr (U_BEFORE >= 0 && finished_in_group<DIR, DENSITY, P::CH>(g, U_BEFORE) &&
+    if constexpr (U_BEFORE >= 0 && finished_in_group<DIR, DENSITY, P::CH, cross_finish<P, DIR>()>(g, U_BEFORE) &&
                   S.kin == (FINISH_DELAY < S.len - 1 ? FINISH_DELAY : S.len - 1))
       w.template finish<U_BEFORE>(w.pend);
     if constexpr (S.last && S.j == G.n - 1) {
-      if constexpr (finished_in_group<DIR, DENSITY, P::CH>(g, S.u)) w.template finish<S.u>(acc);
+      if constexpr (finished_in_group<DIR, DENSITY, P::CH, cross_finish<P, DIR>()>(g, S.u)) w.template finish<S.u>(acc);
       else w.pend = acc;
     }
   });
@@ -550,6 +585,7 @@ __device__ __forceinline__ float pe_trig(float x, double scale_rev, float scale_
 template <class P, int TILE, int NFREQ, int NVALID>
 __device__ __forceinline__ void pe_tile(typename P::Tile& t, int h, float x0, float x1, float x2) {
   constexpr double INV2PI = 0.15915494309189533576888376337251;
+  float vals[16];
   sfor<16>([&](auto rr) {
     constexpr int rho = decltype(rr)::value;
     constexpr PeFeat A = pe_feat(32 * TILE + acc_row(rho, 0), NFREQ, NVALID);
@@ -572,8 +608,10 @@ __device__ __forceinline__ void pe_tile(typename P::Tile& t, int h, float x0, fl
       const int kind = h ? B.kind : A.kind;
       v = kind == 2 ? trig : kind == 1 ? x : 0.f;
     }
-    P::set(t, rho, v);
+    if constexpr (P::KIND == K_BF16X3) vals[rho] = v;
+    else P::set(t, rho, v);  // (fp32: element-wise keeps the forward's register allocation)
   });
+  if constexpr (P::KIND == K_BF16X3) P::pack16(t, vals);
 }
 
 // fragment-native store of one finished tile (mlp_tables.h, "Training stores"): CH
@@ -688,7 +726,7 @@ struct FwdWave {
   static __host__ __device__ constexpr int group_stores(int g) {
     int s = 0;
     for (int u = 0; u < NUNIT_FWD; ++u)
-      if (finished_in_group<0, DENSITY, P::CH>(g, u)) s += unit_stores(u);
+      if (finished_in_group<0, DENSITY, P::CH, cross_finish<P, 0>()>(g, u)) s += unit_stores(u);
     return s;
   }
 
@@ -715,13 +753,16 @@ struct FwdWave {
         out.b[0] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
         out.b[1] = __builtin_bit_cast(bf16x8, make_uint4(d[4], d[5], d[6], d[7]));
       } else {
+        float v[16];
 #pragma unroll
         for (int rho = 0; rho < 16; ++rho) {
           // ReLU as an integer max on the float bits (negative floats are negative ints)
           const int y = max(__float_as_int(acc[rho]), 0);
           if constexpr (STORE) bits |= (y > 0 ? 1u : 0u) << mask_bit(rho);
-          P::set(out, rho, __int_as_float(y));
+          if constexpr (P::KIND == K_BF16X3) v[rho] = __int_as_float(y);
+          else P::set(out, rho, __int_as_float(y));
         }
+        if constexpr (P::KIND == K_BF16X3) P::pack16(out, v);
       }
       out_arr<L>()[n] = out;
       if constexpr (STORE) {
@@ -742,8 +783,15 @@ struct FwdWave {
           out.b[0] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
           out.b[1] = __builtin_bit_cast(bf16x8, make_uint4(d[4], d[5], d[6], d[7]));
         } else {
+          if constexpr (P::KIND == K_BF16X3) {
+            float v[16];
 #pragma unroll
-          for (int rho = 0; rho < 16; ++rho) P::set(out, rho, acc[rho]);
+            for (int rho = 0; rho < 16; ++rho) v[rho] = acc[rho];
+            P::pack16(out, v);
+          } else {
+#pragma unroll
+            for (int rho = 0; rho < 16; ++rho) P::set(out, rho, acc[rho]);
+          }
         }
         Ha[n] = out;
         if constexpr (STORE) store_tile<P>(a.act, a.nblk, AT_TILES, AT_F + n, wblock, lane, out);
@@ -934,7 +982,7 @@ struct DxWave {
   static __host__ __device__ constexpr int group_stores(int g) {
     int s = 0;
     for (int u = 0; u < NUNIT_BWD; ++u)
-      if (finished_in_group<1, false, P::CH>(g, u)) s += CH;
+      if (finished_in_group<1, false, P::CH, cross_finish<P, 1>()>(g, u)) s += CH;
     return s;
   }
 
@@ -967,8 +1015,14 @@ struct DxWave {
       out.b[0] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
       out.b[1] = __builtin_bit_cast(bf16x8, make_uint4(d[4], d[5], d[6], d[7]));
     } else {
+      float v[16];
 #pragma unroll
-      for (int rho = 0; rho < 16; ++rho) P::set(out, rho, ((w >> mask_bit(rho)) & 1u) ? acc[rho] : 0.f);
+      for (int rho = 0; rho < 16; ++rho) {
+        const float y = ((w >> mask_bit(rho)) & 1u) ? acc[rho] : 0.f;
+        if constexpr (P::KIND == K_BF16X3) v[rho] = y;
+        else P::set(out, rho, y);
+      }
+      if constexpr (P::KIND == K_BF16X3) P::pack16(out, v);
     }
     out_arr<s>()[j] = out;
     constexpr int dzt = dz_tile(s, j);

@@ -22,8 +22,10 @@ import torch
 
 from ._lib import check, lib, ptr, stream_of
 
-F32, BF16 = 0, 1
-DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16}
+F32, BF16, BF16X3 = 0, 1, 2
+# bf16x3: fp32 operands split into bf16 hi + lo, products hi*hi + hi*lo + lo*hi on the bf16
+# MFMA with fp32 accumulation (csrc/mlp.hip PBF3): fp32-class results at bf16-MFMA cost x3
+DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16, "bf16x3": BF16X3}
 
 SCENE_BBOX = ((-1.5, -1.5, -1.5), (1.5, 1.5, 1.5))
 
@@ -32,7 +34,7 @@ def dtype_code(d) -> int:
     if isinstance(d, int):
         return d
     if d not in DTYPES:
-        raise ValueError(f"unsupported MLP dtype {d!r} (fp32 or bf16)")
+        raise ValueError(f"unsupported MLP dtype {d!r} (fp32, bf16 or bf16x3)")
     return DTYPES[d]
 
 

@@ -1,10 +1,10 @@
 """Static checks on the gfx950 code hipcc emits for the MLP kernels (CPU; no GPU needed):
 straight-line forward / dX kernels, every counted `s_waitcnt vmcnt(N)` + `s_barrier` weight
 hand-off covering its LDS-DMA (N <= vector-memory ops issued after the last DMA), and no
-scratch in the training kernels of either precision (one tolerated 8-byte spill pair in the
-fp32 forward).  The hand-off protocol is invisible to the compiler (the DMA is
-inline asm), so a codegen change that reorders or adds stores is caught here, not as a
-race on the GPU.  See tools/asm_check.py."""
+scratch in the training kernels of any precision (the fp32 forward tolerates a spilled
+point xyz + one pair, <= 24 B, reloaded a few times over its ~40k instructions).  The
+hand-off protocol is invisible to the compiler (the DMA is inline asm), so a codegen change
+that reorders or adds stores is caught here, not as a race on the GPU.  See tools/asm_check.py."""
 import os
 import re
 import shutil
@@ -20,18 +20,19 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 @pytest.mark.skipif(shutil.which("/opt/rocm/bin/hipcc") is None, reason="no hipcc")
 def test_mlp_kernels_handoffs_and_registers(capsys):
     import asm_check
-    # every training kernel of both precisions (fp32 is the headline path)
+    # every training kernel of the three precisions (fp32 is the headline path)
     kernels = ["fwd_kernel<nerf::mlp::PBF16, true, false>", "dx_kernel<nerf::mlp::PBF16>", "dw_kernel<nerf::mlp::PBF16>",
-               "fwd_kernel<nerf::mlp::PF32, true, false>", "dx_kernel<nerf::mlp::PF32>", "dw_kernel<nerf::mlp::PF32>"]
+               "fwd_kernel<nerf::mlp::PF32, true, false>", "dx_kernel<nerf::mlp::PF32>", "dw_kernel<nerf::mlp::PF32>",
+               "fwd_kernel<nerf::mlp::PBF3, true, false>", "dx_kernel<nerf::mlp::PBF3>", "dw_kernel<nerf::mlp::PBF3>"]
     with tempfile.TemporaryDirectory() as tmp:
         asm = asm_check.build_asm(tmp, kernels)
     asm_check.check(asm)
     out = capsys.readouterr().out
     # the hand-offs are safe and the straight-line kernels have no loops, in every kernel
     assert not [l for l in out.splitlines() if l.startswith("BAD") and "scratch" not in l], "\n" + out
-    # no scratch, except one 8-byte spill/reload pair outside the main body of the fp32 training
-    # forward (512 VGPRs, one wave per SIMD)
+    # no scratch, except the fp32 training forward's few bytes (512 VGPRs, one wave per SIMD)
     for m in re.finditer(r"BAD scratch (\d+) B in (\S+)", out):
-        assert "fwd_kernelINS0_4PF32ELb1ELb0" in m.group(2) and int(m.group(1)) <= 16, "\n" + out
-    for name in ("fwd_kernelINS0_5PBF16ELb1ELb0", "fwd_kernelINS0_4PF32ELb1ELb0", "dx_kernelINS0_4PF32"):
+        assert "fwd_kernelINS0_4PF32ELb1ELb0" in m.group(2) and int(m.group(1)) <= 24, "\n" + out
+    for name in ("fwd_kernelINS0_5PBF16ELb1ELb0", "fwd_kernelINS0_4PF32ELb1ELb0", "dx_kernelINS0_4PF32",
+                 "fwd_kernelINS0_4PBF3ELb1ELb0", "dx_kernelINS0_4PBF3"):
         assert re.search(name + r".*counted_waits=\d+ unsafe=0", out), "\n" + out

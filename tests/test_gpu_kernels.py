@@ -158,7 +158,7 @@ def test_composite_backward(cuda, ops, O, S):
 
 
 # ---------------------------------------------------------------------------------- MLP
-@pytest.mark.parametrize("dtype,tol", [("fp32", 2e-5), ("bf16", 2e-2)])
+@pytest.mark.parametrize("dtype,tol", [("fp32", 2e-5), ("bf16x3", 2e-5), ("bf16", 2e-2)])
 def test_mlp_forward(golden, cuda, ops, packers, dtype, tol):
     pts = torch.from_numpy(golden["mlp_pts"]).to(cuda)
     vd = torch.from_numpy(golden["mlp_vd"]).to(cuda)
@@ -168,7 +168,7 @@ def test_mlp_forward(golden, cuda, ops, packers, dtype, tol):
         np.testing.assert_allclose(raw.cpu().numpy().reshape(32, 8, 4), golden[key], rtol=0, atol=tol)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16"])
 def test_mlp_forward_large_and_density(cuda, ops, O, packers, seeded_state, dtype):
     g = torch.Generator().manual_seed(11)
     M = 5000  # not a multiple of the tile sizes
@@ -179,7 +179,7 @@ def test_mlp_forward_large_and_density(cuda, ops, O, packers, seeded_state, dtyp
         ref = O.network_forward(p, pts.reshape(M // 10, 10, 3), vd).reshape(M, 4)
         got = ops.mlp(packers["model"], pts.to(cuda), vd.to(cuda), 10, dtype=dtype).cpu()
         dens = ops.mlp(packers["model"], pts.to(cuda), None, 1, dtype=dtype, density_only=True).cpu()
-    tol = 2e-5 if dtype == "fp32" else 2e-2
+    tol = 2e-2 if dtype == "bf16" else 2e-5
     np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=0, atol=tol)
     np.testing.assert_allclose(dens[:, 3].numpy(), ref[:, 3].numpy(), rtol=0, atol=tol)
     assert float(dens[:, :3].abs().max()) == 0.0
@@ -194,7 +194,7 @@ def _oracle_mlp_grads(O, seeded_state, pts, vd, gout, spd, dt):
     return {k[len("model."):]: v.grad.double() for k, v in prm.items()}
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16"])
 def test_mlp_backward(cuda, ops, O, seeded_state, dtype):
     g = torch.Generator().manual_seed(12)
     M = 1000
@@ -212,6 +212,12 @@ def test_mlp_backward(cuda, ops, O, seeded_state, dtype):
         if dtype == "fp32":
             err = float((gg - r).abs().max()) / (float(r.abs().max()) + 1e-12)
             assert err < 1e-4, (name, err)
+        elif dtype == "bf16x3":
+            # ~1e-5 relative pre-activations flip the ReLU masks of the few samples within that
+            # of zero: each an O(1/M) change of single entries (up to 5e-3 of the largest one
+            # measured); in norm the gradient holds to ~1e-3 (the masked test below pins the GEMMs)
+            rel = float((gg - r).norm() / (r.norm() + 1e-12))
+            assert rel < 5e-3, (name, rel)
         else:
             # bf16 activations flip a few ReLU masks (|pre-activation| below bf16 resolution):
             # those entries differ by O(1), so bound the norm error and require alignment
@@ -255,13 +261,14 @@ def _masked_mlp(p, x63, d27, mk):
     return torch.cat([F.linear(hv, *p["rgb_linear"]), alpha], -1)
 
 
-@pytest.mark.parametrize("dtype,M", [("fp32", 20010), ("bf16", 20010), ("bf16", 131101)])
+@pytest.mark.parametrize("dtype,M", [("fp32", 20010), ("bf16x3", 20010), ("bf16", 20010), ("bf16", 131101)])
 def test_mlp_backward_kernel_masks(cuda, ops, O, seeded_state, dtype, M):
     """Many dW sample chunks (the last partial) and a ragged final block, against an fp64
     oracle that takes the kernel's own ReLU masks: at these sizes a few pre-activations sit
     within fp32 rounding of 0, and any two fp32 evaluations (the oracle's own fp32 vs fp64
     included) pick different branches there -- forcing the branches isolates the GEMMs.
-    fp32: 1e-4 of the largest entry; bf16 (operands rounded to 8 bits): 2e-2 in norm."""
+    fp32 and bf16x3 (16-bit split operands; measured <= 1.7e-5): 1e-4 of the largest entry;
+    bf16 (operands rounded to 8 bits): 2e-2 in norm."""
     from nerf_amd._lib import lib, ptr, stream_of
     g = torch.Generator().manual_seed(12)
     spd = 10
@@ -288,17 +295,19 @@ def test_mlp_backward_kernel_masks(cuda, ops, O, seeded_state, dtype, M):
     prm = {k: v.double().clone().requires_grad_(True) for k, v in seeded_state.items() if k.startswith("model.")}
     ref = _masked_mlp(O.split_params(prm, "model"), emb[:, :63], emb[:, 63:], mk)
     (ref * gout.double()).sum().backward()
-    if dtype == "fp32":
+    if dtype != "bf16":
         np.testing.assert_allclose(raw.detach().cpu().double().numpy(), ref.detach().numpy(), rtol=0, atol=1e-4)
+    errs = {}
     for name, prm_g in zip(ops.NET_PARAM_NAMES, params):
         r = prm[f"model.{name}"].grad
         gg = prm_g.grad.cpu().double()
-        if dtype == "fp32":
-            err = float((gg - r).abs().max()) / (float(r.abs().max()) + 1e-30)
+        if dtype != "bf16":
+            err = errs[name] = float((gg - r).abs().max()) / (float(r.abs().max()) + 1e-30)
             assert err < 1e-4, (name, err)
         else:
             rel = float((gg - r).norm() / (r.norm() + 1e-30))
             assert rel < 2e-2, (name, rel)
+    print(f"\n{dtype} M={M} max-entry errors:", {k: f"{v:.2e}" for k, v in errs.items()})
 
 
 # ---------------------------------------------------------------------------------- grid
@@ -348,7 +357,7 @@ def test_image_metrics_match_host_evaluator(cuda, ops, H, W, noise):
     assert abs(ssim - ref_ssim) < 1e-9, (ssim, ref_ssim)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16"])
 def test_mlp_dw_deterministic(cuda, ops, seeded_state, dtype):
     """dW with the workspace (per-item partials, fixed-order reduce) is bit-identical run to
     run and equal, to fp32 summation-order rounding, to the atomic accumulation."""

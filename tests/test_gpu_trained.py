@@ -9,6 +9,11 @@ hierarchical render is pinned at:
     within 1e-4 relative (of each tensor's largest entry, and in norm), with a 1e-8 absolute
     floor: the fine net's alpha-bias gradient is a 6.7e-6 sum of cancelling per-sample terms,
     and a different fp32 summation order moves it by 9e-10 (other entries are 1e-5..1e-1);
+  * bf16x3 MLP (split-bf16 MFMA, opt-in; ~1e-5 relative per dot product, 250x fp32's unit
+    roundoff): every value within 2e-3 (bf16's contract bound, with none of bf16's exclusions)
+    and >= 95 % within 1e-4; gradients within 2e-3 relative.  Measured: render depth 1.2e-4
+    on 1 of 64 rays, 16 silhouette pixels of the 100x100 view up to 1.7e-3, gradients up to
+    1.1e-3 (the near-converged trained net's gradients are sums of cancelling terms);
   * bf16 MLP (opt-in): rgb / depth / acc within 2e-3 absolute on >= 95 % of the values and
     within 3e-2 on all of them, PSNR within 0.05 dB.  Rounding the trained weights OR the
     activations to bf16 alone already moves rgb by up to 4.6e-3 / 5.3e-3 on these rays
@@ -29,7 +34,9 @@ pytestmark = pytest.mark.gpu
 os.environ.setdefault("NERF_AMD_NO_ARGV", "1")
 HERE = os.path.dirname(os.path.abspath(__file__))
 KEYS = ["rgb_map_c", "depth_map_c", "acc_map_c", "rgb_map_f", "depth_map_f", "acc_map_f"]
-TOL = {"fp32": 1e-4, "bf16": 2e-3}
+TOL = {"fp32": 1e-4, "bf16x3": 1e-4, "bf16": 2e-3}
+MAXERR = {"fp32": 1e-4, "bf16x3": 2e-3, "bf16": 3e-2}  # bound on every value
+GRAD_REL = {"fp32": 1e-4, "bf16x3": 2e-3}
 
 
 @pytest.fixture(scope="module")
@@ -72,27 +79,28 @@ def _batch(rays, cuda):
             "far": torch.tensor([6.0], device=cuda)}
 
 
-def _check(out, g2, prefix, tol, keys=KEYS, bf16_max=3e-2):
+def _check(out, g2, prefix, dtype, keys=KEYS, all_max=True):
+    tol = TOL[dtype]
     for k in keys:
         got, ref = out[k].detach().cpu().numpy(), g2[f"{prefix}_{k}"]
-        if tol <= 1e-4:  # fp32: every value
+        if dtype == "fp32":  # every value
             np.testing.assert_allclose(got, ref, rtol=0, atol=tol, err_msg=f"{prefix} {k}")
-        else:  # bf16 (module docstring)
+        else:  # bf16x3 / bf16 (module docstring)
             err = np.abs(got - ref)
             frac = float((err <= tol).mean())
-            assert frac >= 0.95 and (bf16_max is None or err.max() <= bf16_max), (prefix, k, frac, float(err.max()))
+            assert frac >= 0.95 and (not all_max or err.max() <= MAXERR[dtype]), (prefix, k, frac, float(err.max()))
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16"])
 def test_render_perturb0(g2, cuda, stack, dtype):
     cfg, net, r = stack
     net.mlp_dtype = dtype
     with torch.no_grad():
         out = r.render(_batch(g2["rays"], cuda))
-    _check(out, g2, "render0", TOL[dtype])
+    _check(out, g2, "render0", dtype)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16"])
 def test_render_perturb1_injected(g2, cuda, stack, dtype):
     """perturb = 1 with the reference's own uniforms (t_rand [64,64], u [64,128]) injected."""
     from nerf_amd import ops
@@ -110,8 +118,8 @@ def test_render_perturb1_injected(g2, cuda, stack, dtype):
         rgb_f, dep_f, acc_f, _ = ops.composite(raw_f, pdf["z_fine"], rays[:, 3:6], True)
     got = dict(rgb_map_c=rgb_c, depth_map_c=dep_c, acc_map_c=acc_c, rgb_map_f=rgb_f, depth_map_f=dep_f,
                acc_map_f=acc_f)
-    _check(got, g2, "render1", TOL[dtype])
-    if dtype == "fp32":
+    _check(got, g2, "render1", dtype)
+    if dtype != "bf16":
         # the merged fine depths themselves: the kernel's CDF agrees with the reference's to an
         # ulp, and the few samples whose u falls within that ulp of a CDF entry move to the
         # neighbouring bin (their rgb/depth effect is checked above at 1e-4); indices given the
@@ -132,12 +140,14 @@ def _grad_check(net, g2, tag, rel=1e-4):
         assert err < rel * scale or err < 1e-8, (str(name), err / scale)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("tag,n", [("grad64", 64), ("grad4096", 4096)])
-def test_loss_gradients_fp32(g2, cuda, stack, tag, n):
+def test_loss_gradients_fp32(g2, cuda, stack, tag, n, dtype):
     """MSE(c) + MSE(f) and its gradient w.r.t. all 48 tensors through the autograd path
     (no flat buffer): 64 rays and the 4096-ray config-3 batch."""
     from src.train.trainers.nerf import NetworkWrapper
     cfg, net, _ = stack
+    net.mlp_dtype = dtype
     wrapper = NetworkWrapper(net)
     net.zero_grad()
     batch = _batch(g2["rays" if n == 64 else "rays4096"], cuda)
@@ -145,11 +155,11 @@ def test_loss_gradients_fp32(g2, cuda, stack, tag, n):
     _, loss, stats = wrapper(batch)
     loss.backward()
     np.testing.assert_allclose([float(stats["loss_c"]), float(stats["loss_f"])], g2[f"{tag}_loss"], rtol=1e-5)
-    _grad_check(net, g2, tag)
+    _grad_check(net, g2, tag, GRAD_REL[dtype])
     net.zero_grad()
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16"])
 def test_config3_batch_row_subset(g2, cuda, stack, dtype):
     """The whole 4096-ray config-3 batch in one chunk; every 16th ray against the reference's
     render of that subset (rays are independent)."""
@@ -157,7 +167,7 @@ def test_config3_batch_row_subset(g2, cuda, stack, dtype):
     net.mlp_dtype = dtype
     with torch.no_grad():
         out = r.render(_batch(g2["rays4096"], cuda))
-    _check({k: v[::16] for k, v in out.items()}, g2, "cfg3sub", TOL[dtype])
+    _check({k: v[::16] for k, v in out.items()}, g2, "cfg3sub", dtype)
 
 
 def test_training_step_flat_grad_path(g2, cuda, stack):
@@ -218,8 +228,8 @@ def test_render_accelerated_matches_reference(g2, cuda, stack):
     assert out["n_queried"] == int(g2["march_queried"])
 
 
-@pytest.mark.parametrize("dtype,img_tol", [("fp32", 1e-4), ("bf16", 2e-3)])
-def test_heldout_view_psnr(g2, cuda, stack, dtype, img_tol):
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16"])
+def test_heldout_view_psnr(g2, cuda, stack, dtype):
     """A 100x100 held-out view of the procedural scene: the image against the reference's
     render, and PSNR against the analytic ground truth within 0.05 dB of the reference's."""
     from src.datasets.nerf.synthetic import psnr, shade
@@ -235,8 +245,8 @@ def test_heldout_view_psnr(g2, cuda, stack, dtype, img_tol):
     assert abs(p_ours - p_ref) <= 0.05, (p_ours, p_ref)
     # (bf16: a few silhouette pixels of the full view flip between surface and background, so
     # only the fraction within 2e-3 and the PSNR bound the image)
-    _check({"rgb_map_f": out["rgb_map_f"]}, {"view100_rgb_map_f": g2["view100_rgb_map_f"]}, "view100", img_tol,
-           keys=["rgb_map_f"], bf16_max=None)
+    _check({"rgb_map_f": out["rgb_map_f"]}, {"view100_rgb_map_f": g2["view100_rgb_map_f"]}, "view100", dtype,
+           keys=["rgb_map_f"], all_max=dtype != "bf16")
 
 
 def test_bake_slabs_concatenate_to_the_full_grid(g2, cuda, stack):

@@ -12,7 +12,7 @@
   cancelling entries into +-lr steps, and an importance sample whose u sits within an ulp of
   a CDF entry changes bins (volume_renderer.py:117) -- recorded, not asserted.
 * ``test_psnr_fp32_vs_bf16_training``: the same training run (seed-0 init, procedural scene,
-  identical ray streams) with the fp32 and the bf16 MLP; held-out PSNR curve of both
+  identical ray streams) with the fp32, the bf16 and the bf16x3 MLP; held-out PSNR curve of each
   (BASELINE config 3's "PSNR curve").  The two runs are different trajectories, so their PSNR
   difference is training noise (checkpoint differences of +-0.6 dB, either sign), so only the
   mean difference over the curve is bounded (0.5 dB); the north_star's 0.05 dB is about
@@ -120,7 +120,8 @@ def test_psnr_fp32_vs_bf16_training(cuda, steps, every):
         return float(np.mean(ps))
 
     curve = {}
-    for dtype in ("fp32", "bf16"):
+    low = ("bf16", "bf16x3")
+    for dtype in ("fp32",) + low:
         cfg.task_arg.mlp_dtype = dtype
         cfg.task_arg.perturb = 1
         torch.manual_seed(0)
@@ -137,10 +138,13 @@ def test_psnr_fp32_vs_bf16_training(cuda, steps, every):
                 curve[dtype].append((step, heldout(net)))
     cfg.task_arg.mlp_dtype = "fp32"
     cfg.task_arg.perturb = 0
-    summary = {"steps": steps, "rays_per_step": int(cfg.task_arg.train_rays), "heldout_views": 4, "res": 100,
-               "psnr_curve_fp32": curve["fp32"], "psnr_curve_bf16": curve["bf16"],
-               "final_delta_db": curve["bf16"][-1][1] - curve["fp32"][-1][1],
-               "mean_delta_db": float(np.mean([b[1] - a[1] for a, b in zip(curve["fp32"], curve["bf16"])]))}
+    summary = {"steps": steps, "rays_per_step": int(cfg.task_arg.train_rays), "heldout_views": 4, "res": 100}
+    for dt in ("fp32",) + low:
+        summary[f"psnr_curve_{dt}"] = curve[dt]
+    for dt in low:  # keys without a suffix: bf16 (round-2 record format)
+        sfx = "" if dt == "bf16" else f"_{dt}"
+        summary["final_delta_db" + sfx] = curve[dt][-1][1] - curve["fp32"][-1][1]
+        summary["mean_delta_db" + sfx] = float(np.mean([b[1] - a[1] for a, b in zip(curve["fp32"], curve[dt])]))
     print("\nPSNR " + json.dumps(summary))
     out_dir = os.path.join(os.path.dirname(HERE), "gpurun_out")
     if os.path.isdir(out_dir):
@@ -148,6 +152,7 @@ def test_psnr_fp32_vs_bf16_training(cuda, steps, every):
             json.dump(summary, f, indent=1)
     # both runs learn the scene; their curves agree to within the run-to-run noise (checkpoint
     # differences of +-0.6 dB, either sign, were measured: profiles/r2/psnr_fp32_vs_bf16.json)
-    for dt in ("fp32", "bf16"):
+    for dt in ("fp32",) + low:
         assert curve[dt][-1][1] > curve[dt][0][1] + 3.0, summary
     assert abs(summary["mean_delta_db"]) <= 0.5, summary
+    assert abs(summary["mean_delta_db_bf16x3"]) <= 0.5, summary
