@@ -13,8 +13,10 @@ Weights: the reference's seed-0 init (torch.manual_seed(0); Network()).  Data is
 synthetic (no dataset offline).  Rank 0 prints one JSON line.
 
 The headline (``value``, ``dtype`` "fp32") runs the MLP in fp32 MFMA, the reference's own
-precision (nn.Linear fp32, network.py:22-74).  The opt-in bf16 MLP (north_star: rgb/depth
-within 2e-3) is measured in the same run and reported as the nested, labelled ``bf16_line``.
+precision (nn.Linear fp32, network.py:22-74).  Two opt-in MLP precisions are measured in the
+same run and reported as nested, labelled lines: ``bf16x3_line`` (split-bf16 operands, three
+bf16 MFMAs per product, ~1e-5 relative per dot product; priced against 1/3 of the bf16 peak)
+and ``bf16_line`` (north_star: rgb/depth within 2e-3).
 ``vs_baseline`` divides by the reference's per-step op graph run eagerly by PyTorch-ROCm on
 the same GPU at the same MLP dtype and perturb (``baseline``); ``cpu_baseline`` is the same
 graph on the host cores (config 1).
@@ -47,7 +49,8 @@ FLOP_PER_SAMPLE = {"mlp_fwd_train": 2 * 593408, "mlp_fwd": 2 * 593408, "mlp_bwd_
 STORE_ROWS = (79 + 78) * 32
 MLP_IO_BYTES = 12 + 16 + 16
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
-PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+# MI355X dense MFMA (MI355X_MICROARCH.md); bf16x3 spends 3 bf16 MFMAs per fp32 product
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3}
 # HBM-bound sampling / compositing kernels; ops.py counts their algorithmic bytes per launch
 STREAM_KERNELS = ("raygen", "sample_stratified", "sample_pdf", "composite_fwd", "composite_bwd")
 
@@ -58,12 +61,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU per step")
-    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"], help="headline MLP dtype")
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "bf16x3", "fp32"], help="headline MLP dtype")
     ap.add_argument("--images", type=int, default=100)
     ap.add_argument("--res", type=int, default=800)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-eager-baseline", action="store_true")
-    ap.add_argument("--no-second", action="store_true", help="skip the labelled bf16 (or fp32) second line")
+    ap.add_argument("--no-second", action="store_true", help="skip the labelled lines of the other MLP dtypes")
     ap.add_argument("--no-render", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=1024)
     ap.add_argument("--detail-steps", type=int, default=5,
@@ -493,9 +496,9 @@ def eager_gpu_baseline(device, n_rays, dtype, reps=3):
 def main():
     args = parse()
     world, rank, device = setup_dist()
-    second = {"fp32": "bf16", "bf16": "fp32"}[args.dtype]
+    others = [] if args.no_second else [d for d in ("fp32", "bf16x3", "bf16") if d != args.dtype]
     lines = {}
-    for dtype in ([args.dtype] + ([] if args.no_second else [second])):
+    for dtype in [args.dtype] + others:
         log(f"training {dtype}: {args.warmup} warmup + {args.steps} timed steps")
         value, ms_step, roofline, kt, train_stream, (cfg, net, ds) = measure_training(args, world, rank, device, dtype)
         render_s, render_stream, grid = None, None, None
@@ -508,7 +511,8 @@ def main():
                 log(f"{dtype}: grid {grid}")
         eager = None
         if rank == 0 and world == 1 and not args.no_eager_baseline:
-            eager = eager_gpu_baseline(device, args.rays, dtype)
+            # bf16x3 stands in for fp32 arithmetic: its baseline is the reference's fp32 eager step
+            eager = eager_gpu_baseline(device, args.rays, "fp32" if dtype == "bf16x3" else dtype)
             log(f"{dtype}: eager PyTorch-ROCm {eager['value']} rays/s")
         lines[dtype] = {
             "value": round(value, 1), "ms_per_step": round(ms_step, 3), "dtype": dtype,
@@ -550,9 +554,8 @@ def main():
         }
         line.update({k: v for k, v in head.items() if k not in line and k not in ("value", "dtype")})
         line["baseline"] = head["baseline"]
-        if not args.no_second:
-            line[f"{second}_line"] = dict(lines[second], label=f"opt-in {second} MLP (same workload)",
-                                          metric=METRIC, unit="rays/s")
+        for d in others:
+            line[f"{d}_line"] = dict(lines[d], label=f"opt-in {d} MLP (same workload)", metric=METRIC, unit="rays/s")
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1,5 +1,5 @@
 # rocprofv3 evidence for bench.py (round 2): kernel trace + stats of the full bench (fp32
-# headline + bf16 line), then FETCH_SIZE and WRITE_SIZE passes per dtype (each its own run),
+# headline + bf16x3 and bf16 lines), then FETCH_SIZE and WRITE_SIZE passes per dtype (each its own run),
 # then the LDS / MFMA counters of the MLP kernels (fp32), then smoke.
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
@@ -8,7 +8,7 @@ rm -rf $OUT && mkdir -p $OUT
 run() { echo "[$(date +%T)] $*" >> $OUT/progress.log; }
 run trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- python3 bench.py --no-cpu-baseline --no-eager-baseline > $OUT/bench_under_rocprof.log 2>$OUT/bench_under_rocprof.err || exit 1
-for dt in fp32 bf16; do
+for dt in fp32 bf16x3 bf16; do
   run fetch $dt
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch_$dt -o fetch --output-format csv -- python3 bench.py --dtype $dt --no-second --steps 2 --warmup 1 --detail-steps 1 --no-cpu-baseline --no-eager-baseline --no-render > $OUT/fetch_$dt.log 2>&1 || exit 2
   run write $dt
