@@ -93,7 +93,9 @@ int nerf_composite_bwd(const float* raw, const float* z, const float* dirs, int 
  * sample m is viewdirs[dir_index ? dir_index[m] : m / samples_per_dir].
  * bwd: accumulates into grad[nerf_mlp_net_params()] (flat, state_dict order).
  * act / masks / dz are opaque workspaces of nerf_mlp_{act,mask,dz}_bytes(M) bytes written by the
- * training forward (flags & NERF_MLP_STORE) and the dX chain; their layouts are internal. */
+ * training forward (flags & NERF_MLP_STORE) and the dX chain; their layouts are internal.
+ * dtype: 0 = fp32 (fp32 MFMA, the reference's precision), 1 = bf16 (operands rounded to bf16),
+ * 2 = bf16x3 (operands split into bf16 hi + lo, three bf16 MFMAs per product, fp32 accumulation). */
 int64_t nerf_mlp_net_params(void);
 int64_t nerf_mlp_param_offset(int i);
 int64_t nerf_mlp_packed_bytes(int dtype, int dir);
