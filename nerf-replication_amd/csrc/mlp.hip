@@ -47,7 +47,7 @@ struct PF32 {
   static constexpr int WAVES = 4;  // one wave per SIMD (<= 512 VGPR+AGPR)
   static constexpr int ESIZE = 4;
   static constexpr int SPL = 4;    // samples per 16-B lane load (dW GEMM)
-  static constexpr bool FAST_PE = false;  // fp32 parity path: libm-accurate sincosf
+  static constexpr int PE = 1;  // PE_LIBM: the fp32 parity path (pe_trig)
   using Store = float;
   struct Tile { float v[16]; };
   static __device__ __forceinline__ f32x16 mma(uint4 a, const Tile& b, int c, f32x16 acc) {
@@ -91,7 +91,7 @@ struct PBF16 {
   static constexpr int WAVES = 8;  // two waves per SIMD (<= 256 VGPR)
   static constexpr int ESIZE = 2;
   static constexpr int SPL = 8;
-  static constexpr bool FAST_PE = true;   // PE rounded to bf16 anyway: v_sin_f32 after f64 reduction
+  static constexpr int PE = 0;  // PE_FAST: rounded to bf16 anyway
   using Store = __bf16;
   struct Tile { bf16x8 b[2]; };
   static __device__ __forceinline__ f32x16 mma(uint4 a, const Tile& b, int c, f32x16 acc) {
@@ -136,7 +136,7 @@ struct PBF3 {
   static constexpr int WAVES = 4;  // one wave per SIMD (16-VGPR tiles)
   static constexpr int ESIZE = 4;
   static constexpr int SPL = 8;
-  static constexpr bool FAST_PE = false;  // fp32-accurate PE (libm sincosf), then split
+  static constexpr int PE = 2;  // PE_POLY: fp32-accurate to 1.6 ulp, then split
   using Store = __bf16;
   struct Tile { bf16x8 hi[2], lo[2]; };
   static __device__ __forceinline__ f32x16 mma(uint4 a, const Tile& b, int c, f32x16 acc) {
@@ -562,19 +562,45 @@ __host__ __device__ constexpr PeFeat pe_feat(int f, int nfreq, int nvalid) {
   return PeFeat{2, r % 3, k, r >= 3 ? 1 : 0};
 }
 
-// sin or cos of x * 2^k.  FAST: the angle in revolutions, x * (2^k / 2pi) + (cos ? 1/4 : 0),
-// reduced exactly enough in f64 (|x 2^k| < 2^13 rad keeps ~40 fractional bits), then
-// v_sin_f32 on [0,1) revolutions -- far inside bf16 resolution.  Accurate: one libm
-// sincosf of the exact fp32 product x * 2^k (as torch computes x * 2.**k, then sin/cos).
-template <bool FAST>
+// sin or cos of x * 2^k, three forms (P::PE):
+//   PE_FAST (bf16): the angle in revolutions, x * (2^k / 2pi) + (cos ? 1/4 : 0), reduced
+//     exactly enough in f64 (|x 2^k| < 2^13 rad keeps ~40 fractional bits), then v_sin_f32 on
+//     [0,1) revolutions -- far inside bf16 resolution.
+//   PE_LIBM (fp32, the parity path): one libm sincosf of the exact fp32 product x * 2^k (as
+//     torch computes x * 2.**k, then sin/cos).  Its large-argument path costs ~140
+//     instructions per value, 3-5 % of the fp32 forward, but the cheaper forms below move the
+//     4096-ray fine-net L0 gradient 3e-4 from the reference's (a correctly rounded f64 sin
+//     does too; libm sincosf: 5e-5, tools/grad_margin.py) against the 1e-4 contract: the fine
+//     net's highest PE band amplifies sample-position ulps 512x.
+//   PE_POLY (bf16x3, whose own products carry ~1e-5 relative error): the f64 revolution
+//     reduction to the nearest quarter turn, t = q/4 + f with |f| <= 1/8, and a Cephes
+//     sinf / cosf polynomial of theta = 2 pi f in fp32, chosen and signed by q mod 4:
+//     branch-free, ~20 VALU, within 1.6 ulp of sin/cos (forward 12 % faster than libm).
+enum PeMode { PE_FAST = 0, PE_LIBM = 1, PE_POLY = 2 };
+__device__ __forceinline__ float sin_rev_poly(double t) {
+  const double q = __builtin_rint(4.0 * t);
+  const double f = __builtin_fma(q, -0.25, t);
+  const float th = (float)(f * 6.283185307179586476925286766559);
+  const float z = th * th;
+  const float s = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z,
+                                                -1.6666654611e-1f) * z, th, th);
+  const float c = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                                                4.166664568298827e-2f) * z, z, __builtin_fmaf(-0.5f, z, 1.0f));
+  const int qi = (int)q;
+  const float r = (qi & 1) ? c : s;
+  return (qi & 2) ? -r : r;
+}
+
+template <int MODE>
 __device__ __forceinline__ float pe_trig(float x, double scale_rev, float scale_rad, double phase, bool is_cos) {
-  if constexpr (FAST) {
-    const double t = __builtin_fma((double)x, scale_rev, phase);
-    return __builtin_amdgcn_sinf((float)(t - __builtin_floor(t)));
-  } else {
+  if constexpr (MODE == PE_LIBM) {
     float s, c;
     sincosf(x * scale_rad, &s, &c);
     return is_cos ? c : s;
+  } else {
+    const double t = __builtin_fma((double)x, scale_rev, phase);
+    if constexpr (MODE == PE_FAST) return __builtin_amdgcn_sinf((float)(t - __builtin_floor(t)));
+    else return sin_rev_poly(t);
   }
 }
 
@@ -603,7 +629,7 @@ __device__ __forceinline__ void pe_tile(typename P::Tile& t, int h, float x0, fl
         const int k = h ? kb : ka;
         const bool is_cos = h ? (B.cos != 0) : (A.cos != 0);
         const double srev = INV2PI * (double)(1 << k);
-        trig = pe_trig<P::FAST_PE>(x, srev, (float)(1 << k), is_cos ? 0.25 : 0.0, is_cos);
+        trig = pe_trig<P::PE>(x, srev, (float)(1 << k), is_cos ? 0.25 : 0.0, is_cos);
       }
       const int kind = h ? B.kind : A.kind;
       v = kind == 2 ? trig : kind == 1 ? x : 0.f;
