@@ -658,12 +658,34 @@ __host__ __device__ constexpr int64_t block_stride_kib(int ntiles, int ch) {
 
 // fragment-native store of one finished tile (mlp_tables.h, "Training stores"): CH
 // lane-linear 16-byte stores per lane, each wave-instruction writes 1 KiB contiguous
+//
+// Cache policy of the training stores (activations, dZ, masks: written once, read once by a
+// later kernel, gigabytes per launch): 0 plain, 1 nt, 2 sc1.  Measured per launch at 524,288
+// samples (tools/mlp_bench.py --libs, interleaved): nt takes the training forward 5.22 -> 4.94
+// ms (fp32), 0.737 -> 0.667 (bf16), 2.38 -> 2.02 (bf16x3) and dX 4.49 -> 4.35 / 0.692 -> 0.626 /
+// 1.92 -> 1.78; sc1 (drops the line from L2) gains as much on fp32 and less on bf16.
+#ifndef NERF_STORE_POLICY
+#define NERF_STORE_POLICY 1
+#endif
+template <int OFF>
+__device__ __forceinline__ void store16(uint4* p, uint4 v) {
+  const u32x4 w = {v.x, v.y, v.z, v.w};
+  if constexpr (NERF_STORE_POLICY == 1) {
+    __builtin_nontemporal_store(w, (u32x4*)p + OFF / 16);
+  } else if constexpr (NERF_STORE_POLICY == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc1" ::"v"(p), "v"(w), "i"(OFF));
+  } else {
+    p[OFF / 16] = v;
+  }
+}
 template <class P>
 __device__ __forceinline__ void store_tile(void* base, int64_t nblk, int ntiles, int tau, int64_t wblock, int lane,
                                            const typename P::Tile& t) {
   uint4* dst = (uint4*)base + tile_kib(nblk, ntiles, tau, wblock, 0, P::CH) * 64 + lane;
-#pragma unroll
-  for (int c = 0; c < P::CH; ++c) dst[c * 64] = P::chunk(t, c);
+  sfor<P::CH>([&](auto cc) {
+    constexpr int c = decltype(cc)::value;
+    store16<c * 1024>(dst, P::chunk(t, c));
+  });
 }
 
 
@@ -796,8 +818,8 @@ struct FwdWave {
         if constexpr ((n & 1) == 0) mw[n >> 1] = bits;
         else mw[n >> 1] |= bits << 8;
         if constexpr (n == fwd_out_tiles(L) - 1)
-          *mask_slot(a.masks, wblock, L == LV ? 8 : L, lane) =
-              make_uint4(mw[0], mw[1], L == LV ? 0u : mw[2], L == LV ? 0u : mw[3]);
+          store16<0>(mask_slot(a.masks, wblock, L == LV ? 8 : L, lane),
+                     make_uint4(mw[0], mw[1], L == LV ? 0u : mw[2], L == LV ? 0u : mw[3]));
       }
     } else if constexpr (L == LFA) {
       if constexpr (n < 8) {  // feature_linear: no activation
@@ -1335,11 +1357,21 @@ __device__ __forceinline__ void dw_flush_bias(float* grad, int ntile, int nvalid
 // so a K step's act-tile reads are one per-lane base + immediates below 64 KiB
 __host__ __device__ constexpr int dw_slot(const DwJobDesc& d, int q) { return q < d.nd ? d.na + q : q - d.nd; }
 
+// dW's tile stream is read exactly once (each tile-block by one work item), so it is loaded nt
+// (bf16 dW 0.957 -> 0.926 ms, bf16x3 2.05 -> 2.02 at 524,288 samples; fp32 unchanged)
+#ifndef NERF_DW_DMA_NT
+#define NERF_DW_DMA_NT 1
+#endif
+#if NERF_DW_DMA_NT
+#define NERF_DW_DMA_AUX " nt"
+#else
+#define NERF_DW_DMA_AUX ""
+#endif
 // global_load_lds_dwordx4 with a uniform 64-bit base (SGPR pair) + per-lane 32-bit offset
 // (the SADDR form: one VGPR per fetch stream instead of a 64-bit address pair)
 __device__ __forceinline__ void glds16_saddr(const void* sbase, uint32_t voff, uint32_t lds_wave_base) {
   uint32_t saved;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" NERF_DW_DMA_AUX "\n\ts_mov_b32 m0, %0"
                : "=&s"(saved) : "v"(voff), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds_wave_base)) : "memory");
 }
 
