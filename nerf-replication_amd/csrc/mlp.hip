@@ -1289,6 +1289,9 @@ __device__ __forceinline__ float f32_frag(const F32Base& B, int s) {
   static_assert(IMM >= 0 && IMM + 128 * 3 < 65536, "ds_read offset is 16 bits");
   return *(lds_cf*)(uintptr_t)(B.b[s & 3] + (uint32_t)(IMM + 128 * (s >> 2)));
 }
+#ifndef NERF_DW_F32_PIPE
+#define NERF_DW_F32_PIPE 1
+#endif
 __device__ __forceinline__ float dw_frag_f32(const char* tile, int s, int lane) {
   return *(const float*)(tile + dw_f32_lane_off(lane, s & 3) + 128 * (s >> 2));
 }
@@ -1457,7 +1460,65 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
     __builtin_amdgcn_sched_barrier(0);
     if (b + D < b_end) fetch(b + D, buf == 0 ? NBUF - 1 : buf - 1);
     const char* tiles = lds + buf * BUF;
-    if constexpr (P::KIND == K_F32) {
+    if constexpr (P::KIND == K_F32 && NERF_DW_F32_PIPE) {
+      // 16 K steps, fully unrolled, software-pipelined one step deep: step s + 1's fragments
+      // (the dz fragment, the k-tiles' act fragments, the alpha pair) are read before step
+      // s's MFMAs issue, fenced by sched_barrier so hipcc keeps that order (on its own it read
+      // two fragments, waited lgkmcnt(0), issued two MFMAs: every LDS latency exposed).
+      // Every read is one of four per-lane bases (s & 3) + an immediate (< 64 KiB).
+      constexpr int KT = JD.kind == DW_VR ? 9 : JD.kt;
+      constexpr int NF = 1 + KT + (JD.kind == DW_FA ? 2 : 0);
+      const uint32_t region = lds_base + (uint32_t)(buf * BUF);
+      const F32Base Bn = f32_base(region + (uint32_t)(n_lds * TB), lane_off);
+      // act tiles: all of them from slot 0 (immediates t * 4 KiB), or the rgb wave's one
+      const F32Base Ba = f32_base(region + (uint32_t)(vr_rgb ? (9 + wave - 4) * TB : 0), lane_off);
+      F32Base Bal{}, Bw{};
+      if constexpr (JD.kind == DW_FA) {
+        Bal = f32_base(region + (uint32_t)((JD.na + 8) * TB), lane_off);
+        Bw = f32_base(region + (uint32_t)(wave * TB), lane_off);
+      }
+      float fr[2][NF];
+      auto rd = [&](auto ss, float (&f)[NF]) {
+        constexpr int s = decltype(ss)::value;
+        constexpr int SOFF = 128 * (s >> 2);
+        f[0] = f32_frag<SOFF>(Bn, s & 3);
+        if (!vr_rgb) {
+          sfor<KT>([&](auto tt) {
+            constexpr int t = decltype(tt)::value;
+            f[1 + t] = f32_frag<t * TB + SOFF>(Ba, s & 3);
+          });
+        } else {
+          f[1] = f32_frag<SOFF>(Ba, s & 3);
+        }
+        if constexpr (JD.kind == DW_FA) {
+          f[KT + 1] = f32_frag<SOFF>(Bal, s & 3);
+          f[KT + 2] = f32_frag<SOFF>(Bw, s & 3);
+        }
+      };
+      auto mm = [&](const float (&f)[NF]) {
+        dbias += f[0];
+        if (!vr_rgb) {
+          sfor<KT>([&](auto tt) {
+            constexpr int t = decltype(tt)::value;
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(f[0], f[1 + t], acc[t], 0, 0, 0);
+          });
+        } else {
+          acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(f[0], f[1], acc[0], 0, 0, 0);
+        }
+        if constexpr (JD.kind == DW_FA) {
+          if (wave == 0) dbias2 += f[KT + 1];
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(f[KT + 1], f[KT + 2], acc2, 0, 0, 0);
+        }
+      };
+      rd(std::integral_constant<int, 0>{}, fr[0]);
+      sfor<16>([&](auto ss) {
+        constexpr int s = decltype(ss)::value;
+        if constexpr (s + 1 < 16) rd(std::integral_constant<int, s + 1>{}, fr[(s + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(fr[s & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    } else if constexpr (P::KIND == K_F32) {
       // 16 K steps as 4 rounds of 4 (s = 4 a + b): the rounds are a real loop (the bases step
       // by 128 B), so the scheduler's window -- and the fragments it keeps in flight -- is
       // one round, not the whole block
@@ -1930,6 +1991,14 @@ static void dw_items(int dtype, int64_t nblk, int item_off[NDWJOB + 1], int job_
       }
   item_off[0] = 0;
   for (int s = 0; s < NDWJOB; ++s) item_off[s + 1] = item_off[s] + n[job_of[s]];
+#ifdef NERF_DW_DIAG
+  // (diagnostic build only) NERF_DW_ONLY_JOB=j: every item to job j, the others skipped
+  if (const char* e = getenv("NERF_DW_ONLY_JOB")) {
+    const int jj = atoi(e);
+    job_of[0] = jj;  // segments 1.. are empty
+    for (int s = 1; s <= NDWJOB; ++s) item_off[s] = target;
+  }
+#endif
 }
 int64_t nerf_mlp_dw_items(int dtype, int64_t M) {
   int off[NDWJOB + 1], job[NDWJOB];
