@@ -1,14 +1,20 @@
 """The north_star's speed target, measured: the reference's per-step PyTorch-ROCm rays/s (its
 op graph run eagerly on the MI355X -- the oracle restatement of volume_renderer.render +
-network.Network) against this build's training step on the same
-4096-ray batch.  Target: >= 50x (north_star).
+network.Network + MSE + clip_grad_value_(40) + torch.optim.Adam, BASELINE.md section 4, the
+same leg bench.py reports as `baseline`) against this build's training step on the same
+4096-ray batch, at the SAME MLP precision and perturb (1) on both sides.
 
-The test prints both rates (run with -s to see them) and asserts a conservative 20x floor so
-that a regression to an eager-like path cannot pass unnoticed; the measured ratio is
-recorded in DESIGN.md / BASELINE.md.  The eager step is forward + backward only (no
-optimizer), this build's step includes clip + Adam."""
+  * fp32 (the reference's precision): this build's step vs the eager fp32 step.  The fp32
+    MFMA ceiling bounds this ratio at ~17x (176k rays/s at 157.3 TFLOP/s); the
+    test asserts >= 8x (measured 13x in round 2).
+  * bf16 (the north_star's ">= 50x at matched PSNR", test_gpu_trained / DESIGN.md 5): this
+    build's bf16 step vs the faster of eager fp32 and eager bf16 autocast (autocast is
+    host-bound and slower); asserts >= 50x (measured 75x).
+
+Run with -s to see the rates."""
 import json
 import os
+import sys
 import time
 
 import pytest
@@ -17,15 +23,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 RAYS = 4096
-
-
-def _rays(O, n, dev):
-    pose = O.pose_spherical(30.0, -30.0, 4.0)
-    o, d = O.get_rays(800, 800, O.focal_from_angle(800, 0.6911112070083618), pose)
-    idx = torch.randint(0, 800 * 800, (n,), generator=torch.Generator().manual_seed(0))
-    rays = torch.cat([o.reshape(-1, 3)[idx], d.reshape(-1, 3)[idx]], 1)
-    gt = torch.rand(n, 3, generator=torch.Generator().manual_seed(1))
-    return rays.to(dev), gt.to(dev)
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _time(fn, reps, warm=2):
@@ -39,42 +37,43 @@ def _time(fn, reps, warm=2):
     return (time.perf_counter() - t0) / reps
 
 
-def test_speedup_vs_pytorch_rocm_eager(cuda, seeded_state):
+def _build_rate(cuda, dtype):
+    """bench.py's timed step: Trainer.train_step (render perturb 1 + MSE + backward + fused clip
+    40 + Adam) on bench.py's 4096-ray batch."""
+    sys.path.insert(0, ROOT)
+    import bench
     from oracle import nerf_oracle as O
-    os.environ.setdefault("NERF_AMD_NO_ARGV", "1")
-    rays, gt = _rays(O, RAYS, cuda)
-    near, far = torch.tensor([2.0], device=cuda), torch.tensor([6.0], device=cuda)
-
-    # the reference's per-step op graph, eager PyTorch on ROCm (fp32, perturb 0)
-    prm = {k: v.to(cuda).clone().requires_grad_(True) for k, v in seeded_state.items()}
-    C, Fn = O.split_params(prm, "model"), O.split_params(prm, "model_fine")
-
-    def eager():
-        for v in prm.values():
-            v.grad = None
-        ret = O.render(C, Fn, rays, near, far)
-        O.loss_fn(ret, gt)[0].backward()
-
-    t_eager = _time(eager, 3)
-
-    # this build: the training step of bench.py (bf16 MLP, perturb 1, clip + Adam)
     from src.config import cfg
     from src.models import make_network
     from src.train.optimizer import make_optimizer
     from src.train.trainers.make_trainer import make_trainer
     from nerf_amd import ops
-    saved = cfg.task_arg.mlp_dtype
-    cfg.task_arg.mlp_dtype = "bf16"
-    torch.manual_seed(0)
-    net = make_network(cfg)
-    trainer = make_trainer(cfg, net)
-    opt = make_optimizer(cfg, net)
-    batch = {"rays": rays[None], "rgbs": gt[None], "near": ops.device_scalar(2.0, cuda),
-             "far": ops.device_scalar(6.0, cuda)}
-    t_ours = _time(lambda: trainer.train_step(batch, opt), 20, warm=5)
-    cfg.task_arg.mlp_dtype = saved
+    rays, gt = bench._bench_rays(O, RAYS, cuda)
+    saved = (cfg.task_arg.mlp_dtype, cfg.task_arg.perturb)
+    cfg.task_arg.mlp_dtype, cfg.task_arg.perturb = dtype, 1
+    try:
+        torch.manual_seed(0)
+        net = make_network(cfg)
+        trainer = make_trainer(cfg, net)
+        opt = make_optimizer(cfg, net)
+        batch = {"rays": rays[None], "rgbs": gt[None], "near": ops.device_scalar(2.0, cuda),
+                 "far": ops.device_scalar(6.0, cuda)}
+        t = _time(lambda: trainer.train_step(batch, opt), 20, warm=5)
+    finally:
+        cfg.task_arg.mlp_dtype, cfg.task_arg.perturb = saved
+    return RAYS / t
 
-    res = {"rays": RAYS, "pytorch_rocm_eager_rays_per_s": RAYS / t_eager, "build_rays_per_s": RAYS / t_ours,
-           "speedup": t_eager / t_ours}
+
+@pytest.mark.parametrize("dtype,floor", [("fp32", 8.0), ("bf16", 50.0)])
+def test_speedup_vs_pytorch_rocm_eager(cuda, dtype, floor):
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ.setdefault("NERF_AMD_NO_ARGV", "1")
+    eager = bench.eager_gpu_baseline(cuda, RAYS, "fp32", reps=2)["value"]
+    if dtype == "bf16":
+        eager = max(eager, bench.eager_gpu_baseline(cuda, RAYS, "bf16", reps=2)["value"])
+    ours = _build_rate(cuda, dtype)
+    res = {"dtype": dtype, "rays": RAYS, "pytorch_rocm_eager_rays_per_s": eager, "build_rays_per_s": ours,
+           "speedup": ours / eager}
     print("\nSPEEDUP " + json.dumps(res))
-    assert res["speedup"] > 20.0, res
+    assert res["speedup"] >= floor, res
