@@ -1292,6 +1292,14 @@ __device__ __forceinline__ float f32_frag(const F32Base& B, int s) {
 #ifndef NERF_DW_F32_PIPE
 #define NERF_DW_F32_PIPE 1
 #endif
+// step after which the pipelined fp32 K loop issues the next block's DMA (-1: before the loop),
+// waves 4..7 NERF_DW_FETCH_SPLIT steps later (after step 1 / step 5: 5.05 -> 4.95 ms at 524k samples)
+#ifndef NERF_DW_FETCH_STEP
+#define NERF_DW_FETCH_STEP 1
+#endif
+#ifndef NERF_DW_FETCH_SPLIT
+#define NERF_DW_FETCH_SPLIT 4
+#endif
 __device__ __forceinline__ float dw_frag_f32(const char* tile, int s, int lane) {
   return *(const float*)(tile + dw_f32_lane_off(lane, s & 3) + 128 * (s >> 2));
 }
@@ -1458,7 +1466,11 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
     wait_vmcnt_rt(G * younger);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (b + D < b_end) fetch(b + D, buf == 0 ? NBUF - 1 : buf - 1);
+    // fp32 (pipelined): the next block's DMA is issued inside the K loop (NERF_DW_FETCH_STEP), the two
+    // waves of a SIMD (w, w + 4) at different steps, so its ~70 issue slots overlap the partner's MFMAs
+    constexpr bool FETCH_IN_LOOP = P::KIND == K_F32 && NERF_DW_F32_PIPE && NERF_DW_FETCH_STEP >= 0;
+    const int fbuf = buf == 0 ? NBUF - 1 : buf - 1;
+    if (!FETCH_IN_LOOP && b + D < b_end) fetch(b + D, fbuf);
     const char* tiles = lds + buf * BUF;
     if constexpr (P::KIND == K_F32 && NERF_DW_F32_PIPE) {
       // 16 K steps, fully unrolled, software-pipelined one step deep: step s + 1's fragments
@@ -1511,12 +1523,21 @@ __device__ __forceinline__ void dw_job(const DwArgs& a, int64_t b_begin, int64_t
         }
       };
       rd(std::integral_constant<int, 0>{}, fr[0]);
+      const bool fhi = wave >= 4;
       sfor<16>([&](auto ss) {
         constexpr int s = decltype(ss)::value;
         if constexpr (s + 1 < 16) rd(std::integral_constant<int, s + 1>{}, fr[(s + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
         mm(fr[s & 1]);
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (FETCH_IN_LOOP && s == NERF_DW_FETCH_STEP) {
+          if (!fhi && b + D < b_end) fetch(b + D, fbuf);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (FETCH_IN_LOOP && s == NERF_DW_FETCH_STEP + NERF_DW_FETCH_SPLIT) {
+          if (fhi && b + D < b_end) fetch(b + D, fbuf);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       });
     } else if constexpr (P::KIND == K_F32) {
       // 16 K steps as 4 rounds of 4 (s = 4 a + b): the rounds are a real loop (the bases step
