@@ -1970,7 +1970,16 @@ static int cu_count() {
 #ifndef NERF_DW_ITEMS_PER_CU
 #define NERF_DW_ITEMS_PER_CU 2
 #endif
+// fp32 (NERF_DW_COST_TABLE 1, default): each job's measured time with the whole chip to itself
+// (diagnostic build -DNERF_DW_DIAG, NERF_DW_ONLY_JOB=j, tools/gpu_dw_jobs.sh; per mille of the L1
+// job) replaces the model below, which under-priced L5 (measured 1.42x L1, modelled 1.25x) and
+// over-priced the view job (0.79x, modelled 1.13x) and L0: dW 4.94 -> 4.72 ms at 524k samples
+#ifndef NERF_DW_COST_TABLE
+#define NERF_DW_COST_TABLE 1
+#endif
 static int64_t dw_job_cost(int dtype, int j) {
+  static constexpr int64_t MEASURED[NDWJOB] = {332, 1000, 1014, 1021, 1018, 1418, 1024, 1012, 1131, 792};
+  if (dtype == 0 && NERF_DW_COST_TABLE) return MEASURED[j] * 16;
   if (dtype != 0 || !NERF_DW_BALANCE_MFMA) return dw_job_tiles(j);
   const int64_t mfma = 2 * 16 * (j < 8 ? gemm_k_tiles(j) : 9) * 64;
   const int64_t fetch = NERF_DW_LAT_CYCLES + 393 * (int64_t)dw_job_tiles(j);
