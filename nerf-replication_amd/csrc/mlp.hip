@@ -1977,9 +1977,17 @@ static int cu_count() {
 #ifndef NERF_DW_COST_TABLE
 #define NERF_DW_COST_TABLE 1
 #endif
+#ifndef NERF_DW_COST_TABLE_BF
+#define NERF_DW_COST_TABLE_BF 1
+#endif
 static int64_t dw_job_cost(int dtype, int j) {
-  static constexpr int64_t MEASURED[NDWJOB] = {332, 1000, 1014, 1021, 1018, 1418, 1024, 1012, 1131, 792};
-  if (dtype == 0 && NERF_DW_COST_TABLE) return MEASURED[j] * 16;
+  static constexpr int64_t MEASURED[3][NDWJOB] = {{332, 1000, 1014, 1021, 1018, 1418, 1024, 1012, 1131, 792},
+                                                  {560, 1000, 1009, 999, 1009, 1733, 1001, 1012, 1117, 1072},  // (unused)
+                                                  {552, 1000, 1011, 1004, 1004, 1465, 1003, 1007, 1144, 1044}};
+  if (dtype == 0 && NERF_DW_COST_TABLE) return MEASURED[0][j] * 16;
+  // bf16x3 too (2.005 -> 1.943 ms); not bf16, whose jobs all stream HBM at once: its solo timings
+  // (L5 1.73x L1) misprice the shared-bandwidth run (0.914 -> 0.949 ms), the tile count does not
+  if (dtype == 2 && NERF_DW_COST_TABLE_BF) return MEASURED[2][j];
   if (dtype != 0 || !NERF_DW_BALANCE_MFMA) return dw_job_tiles(j);
   const int64_t mfma = 2 * 16 * (j < 8 ? gemm_k_tiles(j) : 9) * 64;
   const int64_t fetch = NERF_DW_LAT_CYCLES + 393 * (int64_t)dw_job_tiles(j);
