@@ -62,6 +62,48 @@ def test_raygen_random_ids_and_rgb(cuda, ops):
     np.testing.assert_array_equal(rgb.cpu().numpy(), imgs.reshape(-1, 3)[pix].cpu().numpy())
 
 
+def test_train_batch_reference_ids(cuda, ops):
+    """a2 with the reference's own draw injected: Dataset.__getitem__ (blender.py:124-131) takes
+    torch.randint(0, N_img*H*W, (n,)) over the flat ray table (blender.py:105-108: img*H*W +
+    j*W + i) and gathers rays and rgb.  The same ids through nerf_raygen (pix + images): rgb
+    bit-exact, o bit-exact, d within 2e-7 (the get_rays matmul's summation order)."""
+    from oracle import nerf_oracle as O
+    H = W = 40
+    cam_x = 0.6911112070083618
+    f = O.focal_from_angle(W, cam_x)
+    poses = torch.stack([O.pose_spherical(float(t), -30.0, 4.0) for t in (-150.0, 10.0, 95.0)])
+    imgs = torch.rand(3, H, W, 3, generator=torch.Generator().manual_seed(5))
+    table_o, table_d = [], []
+    for p in poses:
+        o, d = O.get_rays(H, W, f, p)
+        table_o.append(o.reshape(-1, 3))
+        table_d.append(d.reshape(-1, 3))
+    table = torch.cat([torch.cat(table_o), torch.cat(table_d)], 1)  # [N_img*H*W, 6], reference order
+    torch.manual_seed(7)
+    ids = torch.randint(0, table.shape[0], (4096,))                  # blender.py:126
+    rays, rgb, _ = ops.raygen(poses.to(cuda), H, W, f, pix=ids.to(cuda), images=imgs.to(cuda))
+    ref_rays, ref_rgb = table[ids], imgs.reshape(-1, 3)[ids]
+    np.testing.assert_array_equal(rgb.cpu().numpy(), ref_rgb.numpy())
+    np.testing.assert_array_equal(rays[:, :3].cpu().numpy(), ref_rays[:, :3].numpy())
+    np.testing.assert_allclose(rays[:, 3:].cpu().numpy(), ref_rays[:, 3:].numpy(), rtol=0, atol=2e-7)
+
+
+def test_train_batch_philox_uniform(cuda, ops):
+    """The in-kernel draw replacing torch.randint is uniform over all pixels of all images:
+    chi-square over 64 equal bins of the flat id, 2^20 draws (p > 1e-4), and independent
+    (seed, offset) streams differ."""
+    from scipy import stats
+    poses = torch.eye(4, device=cuda).repeat(4, 1, 1)
+    n_pix = 4 * 100 * 100
+    _, _, pix = ops.raygen(poses, 100, 100, 50.0, n_rays=1 << 20, seed=11, want_pix=True)
+    p = pix.cpu().numpy()
+    assert p.min() >= 0 and p.max() < n_pix
+    counts = np.bincount(p * 64 // n_pix, minlength=64)
+    assert stats.chisquare(counts).pvalue > 1e-4, counts
+    _, _, pix2 = ops.raygen(poses, 100, 100, 50.0, n_rays=1 << 20, seed=11, offset=1, want_pix=True)
+    assert (pix2 != pix).float().mean().item() > 0.99
+
+
 # ---------------------------------------------------------------------------------- stratified
 @pytest.mark.parametrize("perturb", [False, True])
 def test_stratified_bit_exact(golden, cuda, ops, O, perturb):
