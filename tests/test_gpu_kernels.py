@@ -416,6 +416,61 @@ def test_grid_index_bit_exact(golden, cuda, ops):
     np.testing.assert_array_equal(idx.cpu().numpy(), golden["grid_idx"])
 
 
+@pytest.mark.parametrize("density", [0.02, 0.3])
+def test_march_gather_empty_cell_skip_exact(cuda, ops, density):
+    """The march gather skips the steps that provably stay in an empty cell (grid.hip,
+    march_skip_empty).  Against brute force -- the occupancy of EVERY step's point o + t d
+    (volume_renderer.py:298-309: clamp, normalise, x127, truncate) -- the one-round gather with
+    K = all steps emits exactly the occupied (ray, step) pairs, in step order: rays from outside
+    the box and from inside, axis-aligned direction components (d = 0), sparse and dense grids."""
+    from nerf_amd._lib import lib, ptr, stream_of
+    g = torch.Generator().manual_seed(31)
+    res, N = 128, 3000
+    grid = (torch.rand(res, res, res, generator=g) < density)
+    grid[:, :, :40] = False                           # long empty runs
+    o = torch.cat([torch.randn(N // 2, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 4.0]),
+                   torch.rand(N - N // 2, 3, generator=g) * 2 - 1])
+    tgt = torch.rand(N, 3, generator=g) * 2.4 - 1.2
+    d = tgt - o
+    d[::7, 0] = 0.0                                   # axis-aligned components
+    d[::11, 1] = 0.0
+    rays = torch.cat([o, d], 1).float().to(cuda).contiguous()
+    t_table = ops.device_table("arange", 2.0, 6.0, 0.005, cuda)
+    S = t_table.numel()
+    # brute force: every step's point, the lookup of grid_index
+    pts = rays[:, None, :3] + t_table[None, :, None] * rays[:, None, 3:]
+    _, occ = ops.grid_index(pts.reshape(-1, 3), grid.to(cuda), res, want_idx=False)
+    occ = occ.reshape(N, S).bool().cpu()
+    # one gather round, K = S
+    f = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=cuda)  # noqa: E731
+    T, rgb, dep, acc = f(N), f(N, 3), f(N), f(N)
+    nxt, start, off, cnt = (f(N, dt=torch.int32) for _ in range(4))
+    alive, exh = f(N, dt=torch.uint8), f(N, dt=torch.uint8)
+    counters = torch.zeros(2, dtype=torch.int32, device=cuda)
+    cap = int(occ.sum()) + 16
+    out_ray, out_step, out_pts = f(cap, dt=torch.int32), f(cap, dt=torch.int32), f(cap, 3)
+    s = stream_of(rays)
+    L = lib()
+    assert L.nerf_march_init(ptr(T), ptr(rgb), ptr(dep), ptr(acc), ptr(nxt), ptr(alive), ptr(exh), N, s) == 0
+    bb = ops._bbox_arr(ops.SCENE_BBOX)
+    gd = grid.to(device=cuda, dtype=torch.uint8).contiguous()
+    assert L.nerf_march_gather(ptr(rays), N, ptr(t_table), S, ptr(gd), res, bb, S, S, 0.0, ptr(T), ptr(rgb), ptr(dep),
+                               ptr(acc), ptr(nxt), ptr(alive), ptr(exh), ptr(counters), ptr(start), ptr(out_ray),
+                               ptr(out_step), ptr(out_pts), ptr(off), ptr(cnt), cap, s) == 0
+    n_pts = int(counters[0])
+    assert n_pts == int(occ.sum())
+    c, o_ = cnt.cpu(), off.cpu()
+    steps, ray_ids = out_step[:n_pts].cpu(), out_ray[:n_pts].cpu()
+    for r in range(N):
+        want = torch.nonzero(occ[r]).flatten().int()
+        assert int(c[r]) == want.numel(), r
+        got = steps[int(o_[r]):int(o_[r]) + int(c[r])]
+        assert torch.equal(got, want), r
+        assert bool((ray_ids[int(o_[r]):int(o_[r]) + int(c[r])] == r).all())
+    np.testing.assert_array_equal(out_pts[:n_pts].cpu().numpy(),
+                                  pts.cpu()[ray_ids.long(), steps.long()].numpy())
+
+
 def test_adam_matches_torch(cuda, ops):
     g = torch.Generator().manual_seed(3)
     n = 10007

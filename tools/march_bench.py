@@ -32,8 +32,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--lib", default=None, help="alternative build of libnerf_amd.so")
+    ap.add_argument("--schedule", default=None, help="time only this schedule")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
+    from nerf_amd import _lib
+    if args.lib:
+        _lib.LIB_PATH = os.path.abspath(args.lib)
     from nerf_amd import ops
     from src.config import cfg
     from src.datasets.nerf.synthetic import view_poses
@@ -53,6 +58,8 @@ def main():
         variants += [(f"{n}_klow{kl}_t{tsp}", SCHEDULES[n], kl, tsp) for n in ("12x2", "16x2")
                      for kl in (2, 4, 8) for tsp in (0.5, 0.9)]
         for name, sched, kl, tsp in variants:
+            if args.schedule and name != args.schedule:
+                continue
             run = lambda: ops.march(net.model_fine.packer(), rays, 2.0, 6.0, grid, dtype=args.dtype,  # noqa: E731
                                     k_schedule=sched, k_low=kl, t_split=tsp)
             run()
