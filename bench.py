@@ -128,12 +128,19 @@ def build(args, device, dtype):
     return cfg, net, trainer, opt, ds
 
 
-def train_step(cfg, trainer, opt, ds, device):
-    rays, rgbs = ds.sample_batch()
+def next_batch(ds, device):
     from nerf_amd import ops
-    batch = {"rays": rays[None], "rgbs": rgbs[None], "near": ops.device_scalar(2.0, device),
-             "far": ops.device_scalar(6.0, device)}
-    return trainer.train_step(batch, opt)
+    rays, rgbs = ds.sample_batch()
+    return {"rays": rays[None], "rgbs": rgbs[None], "near": ops.device_scalar(2.0, device),
+            "far": ops.device_scalar(6.0, device)}
+
+
+def train_step(cfg, trainer, opt, ds, device):
+    """One training step as Trainer.train runs it: this step's batch was prepared during the
+    previous step (its rays and first-chunk stratified samples overlap that step's gradient
+    all-reduce); the next one is prepared here the same way."""
+    batch = getattr(trainer, "prefetched", None) or trainer.prepare(next_batch(ds, device))
+    return trainer.train_step(batch, opt, prefetch=lambda: next_batch(ds, device))
 
 
 def stream_roofline(ktimes, dtype=None):
@@ -262,47 +269,69 @@ def lego_grid():
     return torch.from_numpy(np.unpackbits(z["packed"])[: int(np.prod(shape))].reshape(shape).astype(bool))
 
 
+def max_over_ranks(t: float, device) -> float:
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        tt = torch.tensor([t], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt)
+    return t
+
+
+def timed_frames(fn, device, reps):
+    """(output of the last call, min over reps of the max-over-ranks wall time)."""
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        fn()
+        times = []
+        for _ in range(reps):
+            if dist.is_initialized():
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            o = fn()
+            torch.cuda.synchronize()
+            times.append(max_over_ranks(time.perf_counter() - t0, device))
+    return o, min(times)
+
+
+def bake_timed(packer, dtype, device, reps):
+    """(grid, s): the res-128 bake (occupancy_grid.py:15-80), one voxel slab per rank +
+    all-gather at N > 1 (src/utils/dist_render.py bake_distributed)."""
+    from nerf_amd import ops
+    from src.utils.dist_render import bake_distributed
+
+    def bake():
+        return bake_distributed(lambda slab: ops.bake(packer, 128, 1.0, dtype=dtype, slab=slab), 128)
+    return timed_frames(bake, device, reps)
+
+
 def grid_times(cfg, net, ds, device, reps=2):
     """BASELINE config 4: the 128^3 x 8-corner occupancy bake (occupancy_grid.py:15-80) and the
     grid-accelerated 800x800 march (render_accelerated, volume_renderer.py:268-357) of test
     view 0 through the reference's own baked lego grid (tests/golden/lego_occupancy_grid.npz,
     packed bits of logs/lego/occupancy_grid.pt).  Weights are the synthetic seed-0 init; the
     bake is also timed with the coarse alpha bias shifted by +1 so that the threshold bites
-    (as the reference-generated res-8 bake golden does)."""
-    import contextlib
-    import io
+    (as the reference-generated res-8 bake golden does).  At N > 1 the frame's rays are dealt
+    to the ranks in interleaved blocks and the bake split in voxel slabs."""
     from nerf_amd import ops
     from src.models.nerf.renderer.volume_renderer import Renderer
+    from src.utils.dist_render import render_distributed
     out = {}
     with torch.no_grad():
         for tag, shift in (("", 0.0), ("_shifted", 1.0)):
             net.model.alpha_linear.bias += shift
-
-            def bake():
-                return ops.bake(net.model.packer(), 128, 1.0, dtype=cfg.task_arg.mlp_dtype)
-            bake()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                grid = bake()
-            torch.cuda.synchronize()
-            out[f"bake_s{tag}"] = round((time.perf_counter() - t0) / reps, 4)
+            grid, t = bake_timed(net.model.packer(), cfg.task_arg.mlp_dtype, device, reps)
+            out[f"bake_s{tag}"] = round(t, 4)
             out[f"bake_occupied{tag}"] = int(grid.sum())
             net.model.alpha_linear.bias -= shift
         r = Renderer(net)
         r.set_occupancy_grid(lego_grid(), device)
         rays, _ = ds.image_rays(0)
         batch = {"rays": rays, "near": ops.device_scalar(2.0, device), "far": ops.device_scalar(6.0, device)}
-        with contextlib.redirect_stdout(io.StringIO()):
-            r.render_accelerated(batch)
-            times = []
-            for _ in range(reps):
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                o = r.render_accelerated(batch)
-                torch.cuda.synchronize()
-                times.append(time.perf_counter() - t0)
-        out["march_s_per_frame"] = round(min(times), 4)
+        o, t = timed_frames(lambda: render_distributed(r, batch, accelerated=True,
+                                                       keys=("rgb_map_f", "depth_map_f", "acc_map_f")), device, reps)
+        out["march_s_per_frame"] = round(t, 4)
         out["march_queried_points"] = int(o["n_queried"])
         out["march_evaluated_points"] = int(o["n_evaluated"])
         out["trained"] = trained_grid_times(cfg, device, reps)
@@ -312,29 +341,25 @@ def grid_times(cfg, net, ds, device, reps=2):
 def trained_grid_times(cfg, device, reps=2):
     """Config 4 on a net where the bake threshold bites and rays terminate: the fixture weights
     trained on the procedural scene (tests/golden/trained_v2.npz, tools/train_teacher.py), its
-    own res-128 bake (occupancy_grid.py), then the grid march of an 800x800 held-out view."""
-    import contextlib
-    import io
+    own res-128 bake (occupancy_grid.py), then the grid march and the hierarchical render of an
+    800x800 held-out view (both split over the ranks at N > 1)."""
     import numpy as np
     from nerf_amd import ops
     from src.datasets.nerf.synthetic import view_poses
     from src.models import make_network
     from src.models.nerf.renderer.volume_renderer import Renderer
     from src.utils.camera import focal_for
+    from src.utils.dist_render import render_distributed
     z = np.load(os.path.join(ROOT, "tests", "golden", "trained_v2.npz"), allow_pickle=False)
     torch.manual_seed(0)
     net = make_network(cfg)
     net.load_state_dict({k: torch.from_numpy(z[k]) for k in z.files}, strict=True)
     net = net.to(device).eval()
     out = {}
+    keys = ("rgb_map_f", "depth_map_f", "acc_map_f")
     with torch.no_grad():
-        ops.bake(net.model.packer(), 128, 1.0, dtype=cfg.task_arg.mlp_dtype)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            grid = ops.bake(net.model.packer(), 128, 1.0, dtype=cfg.task_arg.mlp_dtype)
-        torch.cuda.synchronize()
-        out["bake_s"] = round((time.perf_counter() - t0) / reps, 4)
+        grid, t = bake_timed(net.model.packer(), cfg.task_arg.mlp_dtype, device, reps)
+        out["bake_s"] = round(t, 4)
         out["bake_occupied"] = int(grid.sum())
         r = Renderer(net)
         r.set_occupancy_grid(grid, device)
@@ -342,26 +367,16 @@ def trained_grid_times(cfg, device, reps=2):
         pix = torch.arange(800 * 800, device=device)
         rays, _, _ = ops.raygen(pose.reshape(1, 4, 4), 800, 800, focal_for(800), pix=pix)
         batch = {"rays": rays, "near": ops.device_scalar(2.0, device), "far": ops.device_scalar(6.0, device)}
-        with contextlib.redirect_stdout(io.StringIO()):
-            r.render_accelerated(batch)
-            times = []
-            for _ in range(reps):
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                o = r.render_accelerated(batch)
-                torch.cuda.synchronize()
-                times.append(time.perf_counter() - t0)
-            cfg.task_arg.perturb = 0
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            r.render(batch)
-            torch.cuda.synchronize()
-            out["hierarchical_render_s"] = round(time.perf_counter() - t0, 4)
-            cfg.task_arg.perturb = 1
-    out["march_s_per_frame"] = round(min(times), 4)
-    out["march_queried_points"] = int(o["n_queried"])
-    out["march_evaluated_points"] = int(o["n_evaluated"])
-    out["march_rounds"] = int(o.get("rounds", 0))
+        o, t = timed_frames(lambda: render_distributed(r, batch, accelerated=True, keys=keys), device, reps)
+        out["march_s_per_frame"] = round(t, 4)
+        out["march_queried_points"] = int(o["n_queried"])
+        out["march_evaluated_points"] = int(o["n_evaluated"])
+        out["march_rounds"] = int(o.get("rounds", 0))
+        perturb = cfg.task_arg.perturb
+        cfg.task_arg.perturb = 0
+        _, t = timed_frames(lambda: render_distributed(r, batch, keys=keys), device, 1)
+        out["hierarchical_render_s"] = round(t, 4)
+        cfg.task_arg.perturb = perturb
     return out
 
 
@@ -506,9 +521,8 @@ def main():
         if not args.no_render:
             render_s, render_stream = render_frame_time(cfg, net, ds, device, world)
             log(f"{dtype}: render {render_s:.3f} s/frame")
-            if world == 1:
-                grid = grid_times(cfg, net, ds, device)
-                log(f"{dtype}: grid {grid}")
+            grid = grid_times(cfg, net, ds, device)
+            log(f"{dtype}: grid {grid}")
         eager = None
         if rank == 0 and world == 1 and not args.no_eager_baseline:
             # bf16x3 stands in for fp32 arithmetic: its baseline is the reference's fp32 eager step

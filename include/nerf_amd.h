@@ -29,6 +29,7 @@ extern "C" {
 
 #define NERF_DTYPE_F32 0
 #define NERF_DTYPE_BF16 1
+#define NERF_DTYPE_BF16X3 2 /* fp32 operands split into bf16 hi + lo: three bf16 MFMAs per product */
 
 #define NERF_MLP_STORE 1   /* keep activations + ReLU masks for backward */
 #define NERF_MLP_DENSITY 2 /* sigma only (grid bake) */

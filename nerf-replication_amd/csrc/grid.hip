@@ -170,17 +170,22 @@ __device__ __forceinline__ bool march_occupied(const MarchGatherArgs& a, const f
 // subtract, divide, multiply, truncate: each monotone in fp32), so its preimage is an interval
 // [lo, hi) -- within a few ulps of mn + i w, w = (mx - mn) / (res - 1), open-ended for the
 // boundary cells that also hold the clamped outside -- and the computed p = o + t d is monotone
-// in t.  Every step whose t is below the first exit of the interval SHRUNK by a margin of
-// 1e-3 w (~2.4e-5 here, vs fp32 errors of ~1e-6 in p and in t_exit d) is therefore in the same
-// empty cell, and is skipped; the walk resumes one step at a time near the boundary.  Returns the
-// next step to test (> s).
+// in t.  Every step whose t is below the first exit of the interval SHRUNK by a margin m is
+// therefore in the same empty cell, and is skipped; the walk resumes one step at a time near the
+// boundary.  m = max(1e-3 w, 2^-18 (|o| + 8 |d| + |mn| + |mx|)): 1e-3 w is ~2.4e-5 at res 128, but
+// shrinks as 1/res (2.9e-6 at res 1024), while the fp32 errors of p = o + t d, of the interval
+// bounds and of t_exit d are a few ulps of the coordinates' magnitude (~1e-6 for |o| ~ 4, t <= 6
+// here): the absolute floor keeps the margin >= 8 such ulps at any resolution.  Returns the next
+// step to test (> s).
 __device__ __forceinline__ int march_skip_empty(const MarchGatherArgs& a, const float* ray, int s, const int* cell) {
   // fp32 with approximate reciprocals: the errors (~1e-6 in p) are far inside the margin
   float t_exit = 3.0e38f;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const float d = ray[3 + k];
-    const float mn = a.bb.mn[k], w = (a.bb.mx[k] - mn) * (1.0f / (float)(a.res - 1)), m = 1e-3f * w;
+    const float mn = a.bb.mn[k], w = (a.bb.mx[k] - mn) * (1.0f / (float)(a.res - 1));
+    const float mag = fabsf(ray[k]) + 8.0f * fabsf(d) + fabsf(mn) + fabsf(a.bb.mx[k]);
+    const float m = fmaxf(1e-3f * w, mag * 3.814697265625e-6f);  // 2^-18
     const int i = cell[k];
     const float rd = __builtin_amdgcn_rcpf(d);
     if (d > 0.0f && i < a.res - 1) {          // (at max, clamped: stays while p grows)

@@ -1996,16 +1996,20 @@ static int64_t dw_job_cost(int dtype, int j) {
   const int64_t fetch = NERF_DW_LAT_CYCLES + 393 * (int64_t)dw_job_tiles(j);
   return mfma > fetch ? mfma : fetch;
 }
+constexpr int64_t DW_MIN_BLOCKS = 8;  // 32-sample blocks per dW work item, at least
 static void dw_items(int dtype, int64_t nblk, int item_off[NDWJOB + 1], int job_of[NDWJOB]) {
   static const int cus = cu_count();
   const int target = cus * (dtype == 0 ? NERF_DW_ITEMS_PER_CU : 1);
   int n[NDWJOB];
   int64_t cost = 0;
   for (int j = 0; j < NDWJOB; ++j) cost += dw_job_cost(dtype, j);
+  // a small launch (a 64-ray chunk: 128 blocks) gets few items, each of >= DW_MIN_BLOCKS blocks:
+  // every item adds a 364 KB partial-sum slice that the ordered reduce reads back
+  const int64_t max_items = nblk / DW_MIN_BLOCKS > 1 ? nblk / DW_MIN_BLOCKS : 1;
   int total = 0;
   for (int j = 0; j < NDWJOB; ++j) {
     int64_t k = target * (int64_t)dw_job_cost(dtype, j) / cost;
-    n[j] = (int)(k < 1 ? 1 : k > nblk ? nblk : k);
+    n[j] = (int)(k < 1 ? 1 : k > max_items ? max_items : k);
     total += n[j];
   }
   // the remaining CUs go, one at a time, to the job whose items are the longest
@@ -2013,7 +2017,7 @@ static void dw_items(int dtype, int64_t nblk, int item_off[NDWJOB + 1], int job_
     int best = -1;
     double worst = 0.0;  // (worst = 0 only before the first candidate)
     for (int j = 0; j < NDWJOB; ++j) {
-      if (n[j] >= nblk) continue;
+      if (n[j] >= max_items) continue;
       const double per = (double)dw_job_cost(dtype, j) / n[j];
       if (per > worst) worst = per, best = j;
     }

@@ -453,8 +453,9 @@ class _MLP(torch.autograd.Function):
         g_raw = g_raw.contiguous()
         dz = torch.empty(lib().nerf_mlp_dz_bytes(ctx.dtype, ctx.M), dtype=torch.uint8, device=dev)
         # inside ops.direct_grad() (a training step's loss.backward()), accumulate straight into
-        # the parameters' .grad when they are one flat buffer (the dW kernel adds with atomics):
-        # no zero-fill, no 24 autograd accumulation kernels
+        # the parameters' .grad when they are one flat buffer (the dW partial sums are added in a
+        # fixed order by the reduce kernel, or with atomics when DETERMINISTIC_DW is off): no
+        # zero-fill, no 24 autograd accumulation kernels
         direct = ctx.packer.flat_grad() if _DIRECT_GRAD[0] > 0 else None
         grad = direct if direct is not None else torch.zeros(lib().nerf_mlp_net_params(), device=dev,
                                                               dtype=torch.float32)
@@ -542,7 +543,9 @@ def bake(packer: PackedMLP, res: int, threshold: float, bbox=SCENE_BBOX, dtype=F
     if P < 0:
         raise ValueError(f"bake: bad slab {(x0, x1)} for res {res}")
     grid = torch.zeros(x1 - x0, res, res, device=device, dtype=torch.uint8)
-    if P == 0:
+    if P == 0:  # an empty slab (more ranks than voxel planes)
+        if return_sigma:
+            return grid.bool(), torch.empty(0, device=device), torch.empty(0, 3, device=device)
         return grid.bool()
     pts = torch.empty(P, 3, device=device, dtype=torch.float32)
     s = stream_of(pts)

@@ -5,7 +5,7 @@
     python run.py --type dataset  --cfg_file configs/nerf/lego.yaml
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 run.py --type evaluate ...
 
-Under torch.distributed.run every image is split into contiguous ray blocks, one per GPU,
+Under torch.distributed.run every image's rays are dealt to the GPUs in interleaved 256-ray blocks
 and gathered after rendering (src/utils/dist_render.py); rank 0 evaluates and prints.
 """
 import os

@@ -52,6 +52,29 @@ class Renderer:
         return ops.sample_pdf_bins(bins, weights, N_samples, det, seed=self._seed, offset=off)
 
     # ------------------------------------------------------------------ hierarchical render
+    def _chunk(self, grad):
+        ta = cfg.task_arg
+        return int(ta.chunk_size) if grad else int(ta.get("render_chunk", ta.chunk_size))
+
+    def _stratified_key(self, rays_flat, n, near, far):
+        ta = cfg.task_arg
+        return (rays_flat.data_ptr(), n, id(near), id(far), int(ta.N_samples), float(ta.perturb) > 0.0)
+
+    def prepare(self, batch):
+        """Enqueue the first training chunk's stratified sampling of a batch ahead of its
+        render (volume_renderer.py:160-187 reads no parameter): the trainer issues it before
+        waiting for the previous step's gradient all-reduce, so it runs during the reduction.
+        render() then uses it (same Philox offsets as it would have drawn itself)."""
+        rays = batch["rays"]
+        rays_flat = rays.reshape(-1, 6) if rays.ndim == 3 else rays
+        n = min(self._chunk(True), rays_flat.shape[0])
+        ta = cfg.task_arg
+        o1, o2 = self._next_offsets()
+        z, pts, vd = ops.sample_stratified(rays_flat[:n], batch["near"], batch["far"], int(ta.N_samples),
+                                           float(ta.perturb) > 0.0, seed=self._seed, offset=o1)
+        batch["_stratified0"] = (self._stratified_key(rays_flat, n, batch["near"], batch["far"]), o2, z, pts, vd)
+        return batch
+
     def render(self, batch):
         start = time.time()
         ta = cfg.task_arg
@@ -59,16 +82,20 @@ class Renderer:
         rays_flat = rays.reshape(-1, 6) if rays.ndim == 3 else rays
         near, far = batch["near"], batch["far"]
         grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.net.parameters())
-        chunk = int(ta.chunk_size) if grad else int(ta.get("render_chunk", ta.chunk_size))
+        chunk = self._chunk(grad)
         perturb = float(ta.perturb) > 0.0
         white = bool(ta.white_bkgd)
         n_s, n_i = int(ta.N_samples), int(ta.N_importance)
         outs = {}
+        pre = batch.pop("_stratified0", None) if isinstance(batch, dict) else None
         for i in range(0, rays_flat.shape[0], chunk):
             rc = rays_flat[i:i + chunk]
             rd = rc[:, 3:6]
-            o1, o2 = self._next_offsets()
-            z, pts, vd = ops.sample_stratified(rc, near, far, n_s, perturb, seed=self._seed, offset=o1)
+            if i == 0 and pre is not None and pre[0] == self._stratified_key(rays_flat, rc.shape[0], near, far):
+                _, o2, z, pts, vd = pre  # prepared ahead (prepare)
+            else:
+                o1, o2 = self._next_offsets()
+                z, pts, vd = ops.sample_stratified(rc, near, far, n_s, perturb, seed=self._seed, offset=o1)
             raw_c = self.net(pts, vd, "coarse")
             rgb_c, dep_c, acc_c, w_c = self.raw2outputs(raw_c, z, rd, ta.raw_noise_std, white)
             ret = {"rgb_map_c": rgb_c, "depth_map_c": dep_c, "acc_map_c": acc_c}

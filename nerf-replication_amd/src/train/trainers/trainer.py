@@ -6,9 +6,13 @@ fp32 buffer owned by FusedAdam (1,191,688 values, 4.77 MB) -- is averaged across
 two buckets, one per NeRF: each net's MLP backward reports its finished flat gradient
 (PackedMLP.grad_ready) and that bucket's all-reduce starts at once on the collective
 stream, so the fine net's reduction (its backward runs first) overlaps the coarse net's
-backward.  Initial weights are broadcast from rank 0, as DDP does at construction.  The
-clip_grad_value_(40) of trainer.py:61 is fused into the Adam launch.
+backward.  The next batch's ray generation and stratified sampling (which read no
+parameter) are enqueued before the step waits for the reduction, so they run while it is in
+flight (``train_step(..., prefetch=)``).  Initial weights are broadcast from rank 0, as DDP
+does at construction.  The clip_grad_value_(40) of trainer.py:61 is fused into the Adam
+launch.
 """
+import contextlib
 import datetime
 import time
 
@@ -56,6 +60,18 @@ class GradBuckets:
         for pk in self.packers:
             pk.grad_ready = self._hook
 
+    @contextlib.contextmanager
+    def suspended(self):
+        """No bucket fires inside (a local, un-reduced backward)."""
+        hooks = [pk.grad_ready for pk in self.packers]
+        for pk in self.packers:
+            pk.grad_ready = None
+        try:
+            yield
+        finally:
+            for pk, h in zip(self.packers, hooks):
+                pk.grad_ready = h
+
     def begin(self) -> None:
         """Start of a step: forget forwards whose backward never ran (an aborted step), so a
         net's bucket fires after exactly this step's last chunk."""
@@ -95,6 +111,7 @@ class Trainer:
         self.device = device
         self.global_step = 0
         self.clip_value = 40.0
+        self.prefetched = None
         self.buckets = GradBuckets()
         self.buckets.packers = [m.packer() for m in self.network.modules() if hasattr(m, "packer")]
         if dist_world() > 1:
@@ -104,6 +121,8 @@ class Trainer:
         return {k: torch.mean(v) for k, v in loss_stats.items()}
 
     def to_cuda(self, batch):
+        if batch is None:
+            return None
         out = {}
         for k, v in batch.items():
             if torch.is_tensor(v):
@@ -114,31 +133,59 @@ class Trainer:
                 out[k] = v
         return out
 
-    def train_step(self, batch, optimizer):
-        """render -> loss -> backward -> all-reduce -> fused clip + Adam. Returns (loss, stats)."""
+    def prepare(self, batch):
+        """Device copy of a batch with its first render chunk's stratified samples computed
+        (Renderer.prepare): work that reads no parameter, so it may run before the previous
+        step's optimizer update."""
+        batch = self.to_cuda(batch)
+        renderer = getattr(self.network, "renderer", None)
+        if batch is not None and renderer is not None and hasattr(renderer, "prepare"):
+            renderer.prepare(batch)
+        return batch
+
+    def forward_backward(self, batch, optimizer):
+        """render -> loss -> backward, dW straight into FusedAdam's flat .grad; the per-net
+        all-reduce buckets start inside (trainer.py:53-60 of the reference)."""
         from nerf_amd import ops
         self.buckets.begin()
         output, loss, loss_stats = self.network(batch)
         loss = loss.mean()
         optimizer.zero_grad()
-        # dW straight into FusedAdam's flat .grad; per-net all-reduce buckets start inside
         with ops.direct_grad():
             loss.backward()
+        return output, loss, loss_stats
+
+    def apply(self, optimizer):
+        """Wait for the gradient buckets, then fused clip_grad_value_(40) + Adam (:61-62)."""
         self.buckets.finish(optimizer)
         optimizer.clip_value = self.clip_value
         optimizer.step()
+
+    def train_step(self, batch, optimizer, prefetch=None):
+        """One step.  ``prefetch`` (optional) returns the next batch: it is called after the
+        backward has been enqueued and before the step waits for the gradient all-reduce, and
+        the prepared batch (its rays and first chunk's stratified samples enqueued on the
+        compute stream, overlapping the reduction) is left in ``self.prefetched``."""
+        output, loss, loss_stats = self.forward_backward(batch, optimizer)
+        self.prefetched = self.prepare(prefetch()) if prefetch is not None else None
+        self.apply(optimizer)
         return output, loss, loss_stats
 
     def train(self, epoch, data_loader, optimizer, recorder):
         max_iter = len(data_loader)
         self.network.train()
         end = time.time()
-        for iteration, batch in enumerate(data_loader):
+        it = iter(data_loader)
+        batch = next(it, None)
+        if batch is not None:
+            batch = self.prepare(batch)
+        iteration = 0
+        while batch is not None:
             data_time = time.time() - end
-            iteration = iteration + 1
-            batch = self.to_cuda(batch)
+            iteration += 1
             batch["step"] = self.global_step
-            _, loss, loss_stats = self.train_step(batch, optimizer)
+            _, loss, loss_stats = self.train_step(batch, optimizer, prefetch=lambda: next(it, None))
+            batch = self.prefetched
             self.global_step += 1
             if self.local_rank > 0:
                 continue

@@ -1,7 +1,11 @@
-"""Multi-GPU inference: one image's rays split into contiguous row blocks, one per rank,
-rendered independently, then gathered (640,000 rays / 8 = 80,000 per GPU;
-rgb/depth/acc gathered at the end, no other collective).  The grid bake likewise: one voxel
-slab per rank (16 x 128 x 128 at 8 ranks), then an all-gather of the bool grid (2 MB).
+"""Multi-GPU inference: one image's rays dealt to the ranks in interleaved blocks (block b
+to rank b mod W), rendered independently, then gathered (640,000 rays / 8 =
+80,000 per GPU; rgb/depth/acc gathered at the end, no other collective).  Interleaving keeps
+the ranks' work equal when it is not uniform over the image: the grid march
+(render_accelerated, volume_renderer.py:268-357) queries the MLP only where rays cross
+occupied cells, which cluster in the central rows, so contiguous row blocks would leave the
+middle ranks with most of the frame.  The grid bake: one voxel slab per rank (16 x 128 x 128
+at 8 ranks), then an all-gather of the bool grid (2 MB).
 
 Used by run.py --type evaluate|network under torch.distributed.run; the renderer is any
 object with render / render_accelerated (the reference's Renderer interface)."""
@@ -18,12 +22,23 @@ def shard_bounds(n: int, rank: int, world: int):
     return n * rank // world, n * (rank + 1) // world
 
 
-def render_distributed(renderer, batch, accelerated: bool = False, keys=None):
+RAY_BLOCK = 256  # rays per dealt block (640,000-ray frame: 2,500 blocks, 312-313 per rank at 8)
+
+
+def interleaved_index(n: int, rank: int, world: int, block: int = RAY_BLOCK, device=None):
+    """Ray ids of rank's share: blocks b = rank, rank + W, ... of ``block`` consecutive rays."""
+    nb = (n + block - 1) // block
+    blocks = torch.arange(rank, nb, world, device=device)
+    idx = (blocks[:, None] * block + torch.arange(block, device=device)[None]).reshape(-1)
+    return idx[idx < n]
+
+
+def render_distributed(renderer, batch, accelerated: bool = False, keys=None, block: int = RAY_BLOCK):
     """Render batch['rays'] split across ranks; every rank returns the full outputs.
 
-    Each rank renders rays [n r / W, n (r + 1) / W); per-ray outputs ([N] or [N, c]
-    tensors) are padded to the largest share and all_gathered, then trimmed; scalars
-    (render_time, n_queried) are max- / sum-reduced."""
+    Rank r renders the rays of interleaved_index(n, r, W, block); per-ray outputs ([N] or
+    [N, c] tensors) are padded to the largest share, all_gathered and scattered back to ray
+    order; scalars (render_time, n_queried) are max- / sum-reduced."""
     world = _world()
     fn = renderer.render_accelerated if accelerated else renderer.render
     if world == 1:
@@ -32,22 +47,27 @@ def render_distributed(renderer, batch, accelerated: bool = False, keys=None):
     rays = batch["rays"]
     flat = rays.reshape(-1, 6)
     n = flat.shape[0]
-    a, b = shard_bounds(n, rank, world)
+    idx = [interleaved_index(n, r, world, block, flat.device) for r in range(world)]
+    mine = idx[rank]
     sub = dict(batch)
-    sub["rays"] = flat[a:b][None] if rays.dim() == 3 else flat[a:b]
+    own = flat.index_select(0, mine)
+    sub["rays"] = own[None] if rays.dim() == 3 else own
     out = fn(sub)
-    share = (n + world - 1) // world
+    share = max(int(i.numel()) for i in idx)
     res = {}
     for k, v in out.items():
-        if keys is not None and k not in keys:
-            continue
-        if torch.is_tensor(v) and v.dim() >= 1 and v.shape[0] == b - a:
+        per_ray = torch.is_tensor(v) and v.dim() >= 1 and v.shape[0] == mine.numel()
+        if per_ray and keys is not None and k not in keys:
+            continue  # (keys selects the gathered per-ray outputs; scalars are always reduced)
+        if per_ray:
             pad = torch.zeros((share,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
-            pad[: b - a] = v
+            pad[: mine.numel()] = v
             parts = [torch.empty_like(pad) for _ in range(world)]
             dist.all_gather(parts, pad)
-            res[k] = torch.cat([parts[r][: shard_bounds(n, r, world)[1] - shard_bounds(n, r, world)[0]]
-                                for r in range(world)], 0)
+            full = torch.empty((n,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+            for r in range(world):
+                full[idx[r].to(v.device)] = parts[r][: idx[r].numel()]
+            res[k] = full
         elif isinstance(v, (int, float)):
             dev = flat.device if flat.device.type != "cpu" or dist.get_backend() == "gloo" else "cuda"
             t = torch.tensor([float(v)], dtype=torch.float64, device=dev)

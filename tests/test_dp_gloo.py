@@ -26,8 +26,12 @@ def _free_port():
 class _FakeRenderer:
     """rgb / depth / acc as fixed functions of each ray (the split/gather logic under test)."""
 
+    def __init__(self):
+        self.seen = []
+
     def render(self, batch):
         r = batch["rays"].reshape(-1, 6)
+        self.seen.append(r[:, 0].clone())
         return {"rgb_map_f": r[:, :3] * 2.0, "depth_map_f": r[:, 3] + 1.0, "acc_map_f": r[:, 4],
                 "n_queried": int(r.shape[0])}
 
@@ -99,12 +103,17 @@ def _worker(rank, world, port, q):
     all_seeds = [torch.zeros_like(seeds) for _ in range(world)]
     dist.all_gather(all_seeds, seeds)
     seeds_distinct = len({tuple(s.tolist()) for s in all_seeds}) == world
-    # tile-split inference: 1001 rays over the ranks, gathered everywhere
-    from src.utils.dist_render import render_distributed
+    # tile-split inference: 1001 rays over the ranks in interleaved 256-ray blocks (rank r
+    # renders blocks r, r + W, ...), gathered everywhere in ray order
+    from src.utils.dist_render import interleaved_index, render_distributed
     rays = torch.arange(1001 * 6, dtype=torch.float32).reshape(1, 1001, 6)
     full = _FakeRenderer().render({"rays": rays})
-    got = render_distributed(_FakeRenderer(), {"rays": rays})
+    fr = _FakeRenderer()
+    got = render_distributed(fr, {"rays": rays})
     ok = all(torch.equal(got[k], full[k]) for k in ("rgb_map_f", "depth_map_f", "acc_map_f"))
+    mine = interleaved_index(1001, rank, world)
+    ok = ok and len(fr.seen) == 1 and torch.equal(fr.seen[0], rays[0, mine, 0])
+    ok = ok and int(mine[0]) == 256 * rank and (mine // 256 % world == rank).all().item()
     q.put((rank, opt_grad_plain, float(lin.weight.sum()), bucket_grad, ok and got["n_queried"] == 1001,
            two_chunk_ok, seeds_distinct))
     dist.destroy_process_group()
@@ -129,6 +138,24 @@ def test_two_rank_gradient_average_and_broadcast():
         assert render_ok  # tile-split render == single-process render
         assert two_chunk_ok  # one bucket per net after its last chunk; == the flat average
         assert seeds_distinct  # every rank draws its own rays
+
+
+def test_interleaved_split_balances_a_central_workload():
+    """SURVEY.md 8e / render_accelerated: the march's work sits in the rows that cross the
+    occupied cells.  With the work of an 800x800 frame concentrated in its central rows, the
+    busiest of 8 ranks gets <= 2 % above the mean share by interleaved blocks, against >= 2x by
+    contiguous row blocks; every ray is rendered exactly once."""
+    from src.utils.dist_render import interleaved_index, shard_bounds
+    H = W = 800
+    n, world = H * W, 8
+    row = torch.arange(n) // W
+    work = torch.exp(-((row.float() - 400.0) / 120.0) ** 2)  # central rows hold the occupied cells
+    mean = float(work.sum()) / world
+    idx = [interleaved_index(n, r, world) for r in range(world)]
+    assert torch.equal(torch.sort(torch.cat(idx)).values, torch.arange(n))
+    inter = max(float(work[i].sum()) for i in idx) / mean
+    contig = max(float(work[slice(*shard_bounds(n, r, world))].sum()) for r in range(world)) / mean
+    assert inter <= 1.02 and contig >= 2.0, (inter, contig)
 
 
 def _fake_bake_slab(res):
