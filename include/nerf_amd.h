@@ -109,6 +109,11 @@ int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void*
 int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const float* viewdirs, int samples_per_dir,
                  const int32_t* dir_index, int64_t M, int flags, float* raw, void* act, uint16_t* masks,
                  hipStream_t stream);
+/* Inference forward whose sample count lives on the device: M = min(*M_dev, M_cap) is read by the
+ * kernel (a persistent grid loops over the sample blocks), so a producer kernel's count -- the grid
+ * march's gather -- sizes the launch without a host round trip.  raw: [M_cap,4]. */
+int nerf_mlp_fwd_count(const void* packed_fwd, int dtype, const float* pts, const float* viewdirs, int samples_per_dir,
+                       const int32_t* dir_index, const int32_t* M_dev, int64_t M_cap, float* raw, hipStream_t stream);
 int nerf_mlp_bwd(const void* packed_bwd, int dtype, const float* d_raw, int64_t M, const void* act,
                  const uint16_t* masks, void* dz, float* grad, hipStream_t stream);
 /* the two halves of nerf_mlp_bwd (dX chain kernel, dW/db GEMM kernel) as separate calls */
@@ -153,20 +158,26 @@ int nerf_bake_reduce_slab(const float* raw, int res, int dedup, int x0, int x1, 
                           hipStream_t stream);
 
 /* ---- (a12) grid-accelerated march (render_accelerated, volume_renderer.py:268-357) --------------
- * Round structure: init; repeat { zero counters; gather (<= K occupied steps per alive ray,
- * compacted points; a ray whose T < t_split gathers at most k_low; cap = room for points, K <= cap <= INT32_MAX -- size it alive rays x K, a ray
- * that finds no room keeps its position for the next round); fine MLP on the points; composite
- * (stops at T < t_thresh; consumed (nullable, uint64) += the points composited, i.e. the
- * reference's MLP queries -- points gathered past a ray's termination are dropped) } until no
- * ray is alive; finish (white background). */
+ * Round structure: init; repeat { zero counters[0..1]; gather (<= K occupied steps per alive ray,
+ * compacted points; a ray whose T < t_split gathers at most k_low; cap = room for points,
+ * K <= cap <= INT32_MAX; a ray that finds no room keeps its position for the next round, and
+ * every position below min(counters[0], cap) still holds a valid point; evaluated (nullable,
+ * uint64) += that count); fine MLP on the points (nerf_mlp_fwd_count with M_dev = counters: no
+ * host sync); composite (stops at T < t_thresh; consumed (nullable, uint64) += the points
+ * composited, i.e. the reference's MLP queries -- points gathered past a ray's termination are
+ * dropped) } until counters[1] (rays alive entering a round) is 0; finish (white background). */
 int nerf_march_init(float* T, float* rgb, float* depth, float* acc, int32_t* next_step, uint8_t* alive,
                     uint8_t* exhausted, int64_t N, hipStream_t stream);
+/* macro occupancy of 8^3 cell blocks (nullable input of the gather: an empty block is crossed in
+ * one skip; exact, like the cell-level skip) */
+int64_t nerf_march_macro_bytes(int res);
+int nerf_march_macro(const uint8_t* grid, int res, uint8_t* macro, hipStream_t stream);
 int nerf_march_gather(const float* rays, int64_t N, const float* t_table, int n_steps, const uint8_t* grid, int res,
-                      const float* bbox_host, int K, int k_low, float t_split, float* T, float* rgb, float* depth,
-                      float* acc,
-                      int32_t* next_step, uint8_t* alive, uint8_t* exhausted, int32_t* counters,
-                      int32_t* start_step_scratch, int32_t* out_ray, int32_t* out_step, float* out_pts,
-                      int32_t* ray_off, int32_t* ray_cnt, int64_t cap, hipStream_t stream);
+                      const uint8_t* macro, const float* bbox_host, int K, int k_low, float t_split, float* T,
+                      float* rgb, float* depth,
+                      float* acc, int32_t* next_step, uint8_t* alive, uint8_t* exhausted, int32_t* counters,
+                      unsigned long long* evaluated, int32_t* start_step_scratch, int32_t* out_ray, int32_t* out_step,
+                      float* out_pts, int32_t* ray_off, int32_t* ray_cnt, int64_t cap, hipStream_t stream);
 int nerf_march_composite(const float* raw, const float* rays, int64_t N, const float* t_table, const int32_t* ray_off,
                          const int32_t* ray_cnt, const int32_t* out_step, float* T, float* rgb, float* depth,
                          float* acc, int32_t* next_step, uint8_t* alive, uint8_t* exhausted, float step_size,

@@ -141,12 +141,14 @@ struct MarchGatherArgs {
   int n_steps;
   const uint8_t* grid;
   int res;
+  const uint8_t* macro;  // [mres^3] 1 = some cell of the 8^3 block occupied (nerf_march_macro), or null
   BBox bb;
   int K;
   int k_low;       // rays with T < t_split gather at most k_low steps (they terminate soon)
   float t_split;
   MarchState st;
-  int32_t* counters;   // [0] points written, [1] rays alive after gather
+  int32_t* counters;   // [0] points reserved, [1] rays alive entering the round
+  unsigned long long* evaluated;  // += points written below cap (what the MLP evaluates), or null
   int32_t* out_ray;    // [cap]
   int32_t* out_step;   // [cap]
   float* out_pts;      // [cap,3]
@@ -177,7 +179,14 @@ __device__ __forceinline__ bool march_occupied(const MarchGatherArgs& a, const f
 // bounds and of t_exit d are a few ulps of the coordinates' magnitude (~1e-6 for |o| ~ 4, t <= 6
 // here): the absolute floor keeps the margin >= 8 such ulps at any resolution.  Returns the next
 // step to test (> s).
-__device__ __forceinline__ int march_skip_empty(const MarchGatherArgs& a, const float* ray, int s, const int* cell) {
+//
+// Two levels: when the whole 8^3 block of cells around an empty cell is empty (the macro grid,
+// nerf_march_macro), the interval is the block's -- cells [8 j, 8 j + 7] along each axis, the
+// same monotone argument over a union of cells -- so a ray crosses empty space ~8x faster (the
+// walk is a chain of dependent lookups: its length, not the lookups, sets a round's gather time).
+constexpr int MACRO = 8;
+__device__ __forceinline__ int march_skip_empty(const MarchGatherArgs& a, const float* ray, int s, const int* cell,
+                                                int span) {
   // fp32 with approximate reciprocals: the errors (~1e-6 in p) are far inside the margin
   float t_exit = 3.0e38f;
 #pragma unroll
@@ -186,12 +195,12 @@ __device__ __forceinline__ int march_skip_empty(const MarchGatherArgs& a, const 
     const float mn = a.bb.mn[k], w = (a.bb.mx[k] - mn) * (1.0f / (float)(a.res - 1));
     const float mag = fabsf(ray[k]) + 8.0f * fabsf(d) + fabsf(mn) + fabsf(a.bb.mx[k]);
     const float m = fmaxf(1e-3f * w, mag * 3.814697265625e-6f);  // 2^-18
-    const int i = cell[k];
+    const int lo = cell[k] / span * span, hi = min(lo + span - 1, a.res - 1);  // the interval's cells
     const float rd = __builtin_amdgcn_rcpf(d);
-    if (d > 0.0f && i < a.res - 1) {          // (at max, clamped: stays while p grows)
-      t_exit = fminf(t_exit, (mn + (float)(i + 1) * w - m - ray[k]) * rd);
-    } else if (d < 0.0f && i > 0) {           // (at min, clamped: stays while p falls)
-      t_exit = fminf(t_exit, (mn + (float)i * w + m - ray[k]) * rd);
+    if (d > 0.0f && hi < a.res - 1) {         // (at max, clamped: stays while p grows)
+      t_exit = fminf(t_exit, (mn + (float)(hi + 1) * w - m - ray[k]) * rd);
+    } else if (d < 0.0f && lo > 0) {          // (at min, clamped: stays while p falls)
+      t_exit = fminf(t_exit, (mn + (float)lo * w + m - ray[k]) * rd);
     }
   }
   // last step j > s with t_table[j] < t_exit (steps are ~uniform: estimate, then correct)
@@ -205,6 +214,18 @@ __device__ __forceinline__ int march_skip_empty(const MarchGatherArgs& a, const 
     while (j > s && a.t_table[j] >= t_exit) --j;
   }
   return j + 1;
+}
+
+// the step after an empty cell: the macro block's exit when the block is empty, else the cell's
+__device__ __forceinline__ int march_next_after_empty(const MarchGatherArgs& a, const float* ray, int s,
+                                                      const int* cell) {
+  int span = 1;
+  if (a.macro) {
+    const int mres = (a.res + MACRO - 1) / MACRO;
+    const int64_t j = ((int64_t)(cell[0] / MACRO) * mres + cell[1] / MACRO) * mres + cell[2] / MACRO;
+    if (a.macro[j] == 0) span = MACRO;
+  }
+  return march_skip_empty(a, ray, s, cell, span);
 }
 
 __global__ void march_gather_kernel(MarchGatherArgs a) {
@@ -225,7 +246,7 @@ __global__ void march_gather_kernel(MarchGatherArgs a) {
         ++cnt;
         ++s;
       } else {
-        s = march_skip_empty(a, ray, s, cell);
+        s = march_next_after_empty(a, ray, s, cell);
       }
     }
   }
@@ -239,7 +260,12 @@ __global__ void march_gather_kernel(MarchGatherArgs a) {
   }
   const int wtotal = __shfl(incl, 63, 64);
   int base = 0;
-  if (l == 63 && wtotal > 0) base = atomicAdd(&a.counters[0], wtotal);
+  if (l == 63 && wtotal > 0) {
+    base = atomicAdd(&a.counters[0], wtotal);
+    // the positions of this wave's reservation below cap are all written (by emit)
+    const int64_t below = a.cap - (int64_t)base;
+    if (a.evaluated && below > 0) atomicAdd(a.evaluated, (unsigned long long)(below < wtotal ? below : wtotal));
+  }
   base = __shfl(base, 63, 64);
   const unsigned long long live_mask = __ballot(live);
   if (l == 0 && live_mask) atomicAdd(&a.counters[1], __popcll(live_mask));
@@ -251,10 +277,16 @@ __global__ void march_gather_kernel(MarchGatherArgs a) {
   int pos = base + incl - cnt;
   const bool overflow = (int64_t)pos + cnt > a.cap;
   a.ray_off[r] = pos;
-  a.ray_cnt[r] = overflow ? 0 : cnt;
-  // out of room (the caller sizes cap = alive rays x K, so never taken): the ray keeps its
-  // position and gathers again next round
-  if (overflow) return;
+  // out of room: the ray keeps its position and gathers again next round.  The part of its
+  // reservation below cap is still written by emit (ray_cnt = -that many: not composited), so
+  // that every position below min(points reserved, cap) holds a valid point and ray id -- the
+  // MLP launch sized on the device (nerf_mlp_fwd_count) reads exactly that prefix.
+  if (overflow) {
+    const int64_t room = a.cap - (int64_t)pos;
+    a.ray_cnt[r] = -(int)(room <= 0 ? 0 : room < cnt ? room : cnt);
+    return;
+  }
+  a.ray_cnt[r] = cnt;
   a.st.exhausted[r] = (s >= a.n_steps) ? 1 : 0;
   a.st.next_step[r] = s;
 }
@@ -270,7 +302,8 @@ __global__ void march_emit_kernel(MarchEmitArgs e) {
   const MarchGatherArgs& a = e.g;
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= a.N) return;
-  const int cnt = a.ray_cnt[r];
+  const int c = a.ray_cnt[r];
+  const int cnt = c < 0 ? -c : c;  // (< 0: an overflowing ray's points below cap, written only)
   if (cnt == 0) return;
   const float* ray = a.rays + r * 6;
   int pos = a.ray_off[r];
@@ -287,7 +320,7 @@ __global__ void march_emit_kernel(MarchEmitArgs e) {
       ++k;
       ++s;
     } else {
-      s = march_skip_empty(a, ray, s, cell);
+      s = march_next_after_empty(a, ray, s, cell);
     }
   }
 }
@@ -329,7 +362,8 @@ __global__ void march_composite_kernel(MarchCompArgs a) {
 }
 
 __device__ __forceinline__ int march_composite_ray_impl(const MarchCompArgs& a, int64_t r) {
-  const int cnt = a.ray_cnt[r], off = a.ray_off[r];
+  const int c = a.ray_cnt[r], off = a.ray_off[r];
+  const int cnt = c > 0 ? c : 0;  // (< 0: gathered nothing this round, see march_gather_kernel)
   const float* ray = a.rays + r * 6;
   const float dx = ray[3], dy = ray[4], dz = ray[5];
   const float dist = fmul(a.step_size, sqrtf(fadd(fadd(fmul(dx, dx), fmul(dy, dy)), fmul(dz, dz))));
@@ -365,6 +399,19 @@ __device__ __forceinline__ int march_composite_ray_impl(const MarchCompArgs& a, 
   a.st.acc[r] = acc;
   if (!alive || a.st.exhausted[r]) a.st.alive[r] = 0;
   return used;
+}
+
+// macro occupancy: block (i, j, k) = cells [8 i, 8 i + 8) x [8 j, ..) x [8 k, ..) (clipped at res)
+__global__ void march_macro_kernel(const uint8_t* grid, int res, uint8_t* macro) {
+  const int mres = (res + MACRO - 1) / MACRO;
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= (int64_t)mres * mres * mres) return;
+  const int bi = (int)(b / ((int64_t)mres * mres)), bj = (int)((b / mres) % mres), bk = (int)(b % mres);
+  uint8_t any = 0;
+  for (int i = bi * MACRO; i < min(bi * MACRO + MACRO, res); ++i)
+    for (int j = bj * MACRO; j < min(bj * MACRO + MACRO, res); ++j)
+      for (int k = bk * MACRO; k < min(bk * MACRO + MACRO, res); ++k) any |= grid[((int64_t)i * res + j) * res + k];
+  macro[b] = any ? 1 : 0;
 }
 
 struct MarchInitArgs { MarchState st; int64_t N; };
@@ -465,21 +512,36 @@ int nerf_march_init(float* T, float* rgb, float* depth, float* acc, int32_t* nex
   return check_launch("nerf_march_init");
 }
 
-// counters[0] = points emitted, counters[1] = rays alive entering this round (zero them first).
+// counters[0] = points reserved, counters[1] = rays alive entering this round (zero them first);
+// evaluated (nullable) += the points written, min(points reserved, cap).
 // start_step_scratch: [N] int32 workspace.
+int64_t nerf_march_macro_bytes(int res) {
+  if (res <= 1) return -1;
+  const int64_t m = (res + MACRO - 1) / MACRO;
+  return m * m * m;
+}
+
+int nerf_march_macro(const uint8_t* grid, int res, uint8_t* macro, hipStream_t stream) {
+  NERF_REQUIRE(res > 1, "nerf_march_macro: bad res");
+  NERF_REQUIRE(grid && macro, "nerf_march_macro: null pointer");
+  hipLaunchKernelGGL(march_macro_kernel, grid1(nerf_march_macro_bytes(res)), dim3(256), 0, stream, grid, res, macro);
+  return check_launch("nerf_march_macro");
+}
+
 int nerf_march_gather(const float* rays, int64_t N, const float* t_table, int n_steps, const uint8_t* grid, int res,
-                      const float* bbox_host, int K, int k_low, float t_split, float* T, float* rgb, float* depth,
+                      const uint8_t* macro, const float* bbox_host, int K, int k_low, float t_split, float* T,
+                      float* rgb, float* depth,
                       float* acc,
                       int32_t* next_step, uint8_t* alive, uint8_t* exhausted, int32_t* counters,
-                      int32_t* start_step_scratch, int32_t* out_ray, int32_t* out_step, float* out_pts,
-                      int32_t* ray_off, int32_t* ray_cnt, int64_t cap, hipStream_t stream) {
+                      unsigned long long* evaluated, int32_t* start_step_scratch, int32_t* out_ray, int32_t* out_step,
+                      float* out_pts, int32_t* ray_off, int32_t* ray_cnt, int64_t cap, hipStream_t stream) {
   NERF_REQUIRE(N >= 0 && n_steps >= 0 && K > 0 && res > 1 && bbox_host, "nerf_march_gather: bad arguments");
   NERF_REQUIRE(cap >= K && cap <= INT32_MAX, "nerf_march_gather: need K <= cap <= INT32_MAX (point offsets are int32)");
   if (N == 0) return 0;
   NERF_REQUIRE(k_low > 0, "nerf_march_gather: k_low must be > 0");
-  MarchGatherArgs a{rays, N, t_table, n_steps, grid, res, make_bbox(bbox_host), K, k_low, t_split,
+  MarchGatherArgs a{rays, N, t_table, n_steps, grid, res, macro, make_bbox(bbox_host), K, k_low, t_split,
                     {T, rgb, depth, acc, next_step, alive, exhausted},
-                    counters, out_ray, out_step, out_pts, ray_off, ray_cnt, cap};
+                    counters, evaluated, out_ray, out_step, out_pts, ray_off, ray_cnt, cap};
   if (hipMemcpyAsync(start_step_scratch, next_step, N * sizeof(int32_t), hipMemcpyDeviceToDevice, stream) !=
       hipSuccess) {
     set_error("nerf_march_gather: hipMemcpyAsync failed");

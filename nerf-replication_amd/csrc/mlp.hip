@@ -539,9 +539,14 @@ __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
 // issue the DMA of group G into slot `slot`: every wave issues exactly NF wave-instructions
 // (the last chunk is re-copied by the surplus waves -- identical bytes), so the count a
 // later wait needs is a compile-time constant.
-template <class P, int C0, int NCH>
+template <class P, int C0, int NCH, bool LAUNDER = false>
 __device__ __forceinline__ void fetch_group(const uint4* gsrc, uint32_t slot_base, int wave, int lane) {
   constexpr int NF = (NCH + P::WAVES - 1) / P::WAVES;
+  if constexpr (LAUNDER) {  // (persistent forward: the chunk indices are recomputed per group, not
+    uint32_t w = wave;      // CSE'd across the groups and held -- spilled -- across the block loop)
+    settle(w);
+    wave = (int)w;
+  }
 #pragma unroll
   for (int i = 0; i < NF; ++i) {
     const int k = cmin(wave + P::WAVES * i, NCH - 1);
@@ -715,9 +720,11 @@ struct FwdArgs {
   float* raw;                // [M,4]
   void* act;                 // [AT_TILES][nblk] tile-blocks or null
   void* masks;               // [nblk][MASK_GROUPS][64] x 16 B or null
+  const int32_t* M_dev;      // persistent inference launch: M = min(*M_dev, M_cap), read on the device
+  int64_t M_cap;
 };
 
-template <class P, bool STORE, bool DENSITY>
+template <class P, bool STORE, bool DENSITY, bool PERSIST = false>
 struct FwdWave {
   using Tile = typename P::Tile;
   static constexpr int CH = P::CH;
@@ -737,19 +744,20 @@ struct FwdWave {
   uint4 bias[4];
   f32x16 pend;      // finished accumulator awaiting its deferred finish (group_body)
 
-  __device__ __forceinline__ FwdWave(const FwdArgs& args, const uint4* smem) : a(args), lds(smem) {
+  __device__ __forceinline__ FwdWave(const FwdArgs& args, const uint4* smem, int64_t blk, int tid)
+      : a(args), lds(smem) {
     gw = (const uint4*)a.wpack;
     lds_base = (uint32_t)(uintptr_t)(lds_void*)smem;
-    lane = threadIdx.x & 63;
-    wave = threadIdx.x >> 6;
+    lane = tid & 63;
+    wave = tid >> 6;
     h = lane >> 5;
-    wblock = (int64_t)blockIdx.x * P::WAVES + wave;
+    wblock = blk * P::WAVES + wave;
     m = wblock * 32 + (lane & 31);
   }
 
   template <int g> __device__ __forceinline__ void fetch() {
     constexpr Group G = GT::t.g[g];
-    fetch_group<P, G.c0, G.nch>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
+    fetch_group<P, G.c0, G.nch, PERSIST>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
   }
 
   // input tile t of layer L (mlp_tables.h: Ha/Hb ping-pong, PE tiles X / D)
@@ -960,12 +968,33 @@ __device__ __forceinline__ void young_priority() {
   if (NERF_SETPRIO_YOUNG && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 }
 
-template <class P, bool STORE, bool DENSITY>
+// PERSIST (inference only): the sample count is read on the device (a.M_dev, e.g. the grid
+// march's gather count: no host round trip sizes the launch) and a grid of one wave of
+// workgroups loops over the sample blocks; the barrier at the end of each block keeps the next
+// block's prologue DMA out of the ring slot still being read.
+template <class P, bool STORE, bool DENSITY, bool PERSIST>
 __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
   young_priority();
-  FwdWave<P, STORE, DENSITY> w(a, smem_u4);
-  w.run();
+  if constexpr (!PERSIST) {
+    FwdWave<P, STORE, DENSITY> w(a, smem_u4, blockIdx.x, threadIdx.x);
+    w.run();
+  } else {
+    static_assert(!STORE, "the persistent forward is inference only");
+    const int64_t cnt = a.M_dev[0];
+    FwdArgs b = a;
+    b.M = cnt < a.M_cap ? cnt : a.M_cap;
+    for (int64_t blk = blockIdx.x; blk * samples_per_block<P>() < b.M; blk += gridDim.x) {
+      // the thread id, laundered per block: every lane-dependent address (the weight DMA sources,
+      // the LDS read bases) is then recomputed inside the body, as in the one-block kernel,
+      // instead of being hoisted out of the loop and held in registers across it (spills)
+      int tid = threadIdx.x;
+      asm volatile("" : "+v"(tid));
+      FwdWave<P, STORE, DENSITY, true> w(b, smem_u4, blk, tid);
+      w.run();
+      __syncthreads();
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1787,11 +1816,33 @@ static void allow_lds(K kernel, size_t bytes) {
 
 template <class P, bool STORE, bool DENSITY>
 static void launch_fwd(const FwdArgs& a, hipStream_t stream) {
-  static const bool lds_ok = (allow_lds(fwd_kernel<P, STORE, DENSITY>, fwd_lds_bytes<P>()), true);
+  static const bool lds_ok = (allow_lds(fwd_kernel<P, STORE, DENSITY, false>, fwd_lds_bytes<P>()), true);
   (void)lds_ok;
   const int spb = samples_per_block<P>();
   dim3 grid((unsigned)(STORE ? a.nblk * 32 / spb : (a.M + spb - 1) / spb));
-  hipLaunchKernelGGL((fwd_kernel<P, STORE, DENSITY>), grid, dim3(P::WAVES * 64), fwd_lds_bytes<P>(), stream, a);
+  hipLaunchKernelGGL((fwd_kernel<P, STORE, DENSITY, false>), grid, dim3(P::WAVES * 64), fwd_lds_bytes<P>(), stream,
+                     a);
+}
+
+// persistent inference forward: one wave of workgroups (every CU x its resident workgroups),
+// fewer when M_cap needs fewer blocks
+template <class P>
+static void launch_fwd_persist(const FwdArgs& a, hipStream_t stream) {
+  auto kern = fwd_kernel<P, false, false, true>;
+  static const int resident = [&] {
+    allow_lds(kern, fwd_lds_bytes<P>());
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kern, P::WAVES * 64, fwd_lds_bytes<P>()) !=
+            hipSuccess || per <= 0)
+      per = 1;
+    return cus * per;
+  }();
+  const int64_t spb = samples_per_block<P>(), need = (a.M_cap + spb - 1) / spb;
+  dim3 grid((unsigned)(need < resident ? need : resident));
+  hipLaunchKernelGGL(kern, grid, dim3(P::WAVES * 64), fwd_lds_bytes<P>(), stream, a);
 }
 
 template <class P>
@@ -1827,7 +1878,8 @@ void mlp_fwd_train_impl(const FwdArgs& a, hipStream_t stream) {
 }
 template <class P>
 void mlp_fwd_infer_impl(const FwdArgs& a, bool density, hipStream_t stream) {
-  if (density) launch_fwd<P, false, true>(a, stream);
+  if (a.M_dev) launch_fwd_persist<P>(a, stream);
+  else if (density) launch_fwd<P, false, true>(a, stream);
   else launch_fwd<P, false, false>(a, stream);
 }
 template <class P>
@@ -1944,6 +1996,23 @@ int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const floa
     else mlp_fwd_infer_impl<PBF3>(a, density, stream);
   }
   return check_launch("nerf_mlp_fwd");
+}
+
+// inference forward whose sample count is on the device (min(*M_dev, M_cap)): no host sync sizes
+// the launch (the grid march's rounds)
+int nerf_mlp_fwd_count(const void* packed_fwd, int dtype, const float* pts, const float* viewdirs, int samples_per_dir,
+                       const int32_t* dir_index, const int32_t* M_dev, int64_t M_cap, float* raw, hipStream_t stream) {
+  NERF_REQUIRE(dtype >= 0 && dtype <= 2, "nerf_mlp_fwd_count: bad dtype %d", dtype);
+  NERF_REQUIRE(M_cap >= 0, "nerf_mlp_fwd_count: M_cap < 0");
+  if (M_cap == 0) return 0;
+  NERF_REQUIRE(packed_fwd && pts && raw && viewdirs && M_dev, "nerf_mlp_fwd_count: null pointer");
+  NERF_REQUIRE(dir_index || samples_per_dir > 0, "nerf_mlp_fwd_count: samples_per_dir must be > 0");
+  FwdArgs a{(const char*)packed_fwd, pts, viewdirs, dir_index, samples_per_dir, M_cap, 0, raw, nullptr, nullptr,
+            M_dev, M_cap};
+  if (dtype == 0) mlp_fwd_infer_impl<PF32>(a, false, stream);
+  else if (dtype == 1) mlp_fwd_infer_impl<PBF16>(a, false, stream);
+  else mlp_fwd_infer_impl<PBF3>(a, false, stream);
+  return check_launch("nerf_mlp_fwd_count");
 }
 
 // work items of the dW launch: at most one per CU (a single wave of workgroups that ends

@@ -42,6 +42,7 @@ SIGNATURES = {
     "nerf_mlp_dw_items": (_i64, [_i32, _i64]),
     "nerf_mlp_pack": (_i32, [_p, _i32, _p, _p, _p]),
     "nerf_mlp_fwd": (_i32, [_p, _i32, _p, _p, _i32, _p, _i64, _i32, _p, _p, _p, _p]),
+    "nerf_mlp_fwd_count": (_i32, [_p, _i32, _p, _p, _i32, _p, _p, _i64, _p, _p]),
     "nerf_mlp_bwd": (_i32, [_p, _i32, _p, _i64, _p, _p, _p, _p, _p]),
     "nerf_mlp_bwd_dx": (_i32, [_p, _i32, _p, _i64, _p, _p, _p]),
     "nerf_mlp_bwd_dw": (_i32, [_i32, _i64, _p, _p, _p, _p]),
@@ -55,8 +56,10 @@ SIGNATURES = {
     "nerf_bake_points_slab": (_i32, [_i32, _p, _i32, _i32, _i32, _p, _p]),
     "nerf_bake_reduce_slab": (_i32, [_p, _i32, _i32, _i32, _i32, _f32, _p, _p]),
     "nerf_march_init": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _p]),
-    "nerf_march_gather": (_i32, [_p, _i64, _p, _i32, _p, _i32, _p, _i32, _i32, _f32, _p, _p, _p, _p, _p, _p, _p,
-                                 _p, _p, _p, _p, _p, _p, _p, _i64, _p]),
+    "nerf_march_macro_bytes": (_i64, [_i32]),
+    "nerf_march_macro": (_i32, [_p, _i32, _p, _p]),
+    "nerf_march_gather": (_i32, [_p, _i64, _p, _i32, _p, _i32, _p, _p, _i32, _i32, _f32, _p, _p, _p, _p, _p, _p, _p,
+                                 _p, _p, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "nerf_march_composite": (_i32, [_p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _f32, _f32, _p, _p]),
     "nerf_march_finish": (_i32, [_p, _p, _i64, _i32, _p]),
     "nerf_metrics_workspace_bytes": (_i64, [_i32, _i32]),

@@ -562,26 +562,46 @@ def bake(packer: PackedMLP, res: int, threshold: float, bbox=SCENE_BBOX, dtype=F
 MARCH_POINT_BYTES = 4 + 4 + 12 + 16  # out_ray, out_step, out_pts, raw per gathered point
 
 
+def mlp_count(packer: PackedMLP, pts: torch.Tensor, viewdirs: torch.Tensor, dir_index: torch.Tensor,
+              M_dev: torch.Tensor, raw: torch.Tensor, dtype=F32) -> torch.Tensor:
+    """Inference MLP on the first min(M_dev[0], cap) points, the count read on the device
+    (nerf_mlp_fwd_count): no host round trip sizes the launch.  raw: [cap,4] (output)."""
+    code = dtype_code(dtype)
+    cap = int(raw.shape[0])
+    check(lib().nerf_mlp_fwd_count(ptr(packer.get(code, 0)), code, ptr(pts), ptr(viewdirs), 1, ptr(dir_index),
+                                   ptr(M_dev), cap, ptr(raw), stream_of(pts)), "nerf_mlp_fwd_count")
+    return raw
+
+
 def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: torch.Tensor, step_size: float = 0.005,
           t_thresh: float = 1e-4, bbox=SCENE_BBOX, white_bkgd: bool = True, dtype=F32,
           t_table: Optional[torch.Tensor] = None, k_schedule=(12, 24, 48, 96, 192, 384, 768),
-          round_bytes: int = 1 << 31, k_low: int = 8, t_split: float = 0.9):
+          round_bytes: int = 1 << 31, k_low: int = 8, t_split: float = 0.9, sync_every: int = 4,
+          use_macro: bool = True):
     """Grid-accelerated march with early termination -> dict(rgb_map_f, depth_map_f,
     acc_map_f, n_queried, n_evaluated, rounds).
 
-    Each round gathers up to K occupied steps of every alive ray and evaluates them in one MLP
-    launch; compositing stops at T < t_thresh, so points past a ray's termination were
-    evaluated speculatively; a ray whose transmittance is already below t_split gathers at most
-    k_low steps (it is about to terminate; on the trained fixture net's 800x800 view this cut the
-    speculative evaluations from 48 % to 6 % of the queries and the frame from 0.166 to 0.127 s,
-    profiles/r2/march_sweep.json).  n_queried counts the composited points only -- exactly the
-    reference's MLP queries (volume_renderer.py:324) -- and n_evaluated every point the MLP ran
-    on.  A round's point buffers are sized alive rays x K, with K capped so they stay within
-    round_bytes (and int32 offsets)."""
+    Each round gathers up to K occupied steps of every alive ray into one point buffer of
+    ``cap`` points (round_bytes / MARCH_POINT_BYTES, <= INT32_MAX), evaluates them in one MLP
+    launch and composites them; compositing stops at T < t_thresh, so points past a ray's
+    termination were evaluated speculatively; a ray whose transmittance is already below
+    t_split gathers at most k_low steps (it is about to terminate; on the trained fixture net's
+    800x800 view this cut the speculative evaluations from 48 % to 6 % of the queries,
+    profiles/r2/march_sweep.json).  The rounds run without host round trips: the MLP reads the
+    gather's point count on the device (mlp_count), a ray that finds no room in the buffer
+    gathers again next round, and the host checks for live rays every ``sync_every`` rounds
+    (rounds after the last live one find nothing and cost a few empty launches).  The walk
+    skips empty cells, and whole empty 8^3 blocks of cells (use_macro), exactly.  n_queried
+    counts the composited points only -- exactly the reference's MLP queries
+    (volume_renderer.py:324) -- and n_evaluated every point the MLP ran on."""
     rays = _f32c(rays.reshape(-1, 6), "rays")
     dev, N = rays.device, rays.shape[0]
     L = lib()
     s = stream_of(rays)
+    if N == 0:
+        z = torch.zeros(0, device=dev)
+        return {"rgb_map_f": torch.zeros(0, 3, device=dev), "depth_map_f": z, "acc_map_f": z.clone(), "n_queried": 0,
+                "n_evaluated": 0, "rounds": 0}
     if t_table is None:
         t_table = device_table("arange", float(near), float(far), float(step_size), dev)
     t_table = _f32c(t_table.to(dev), "t_table")
@@ -599,42 +619,45 @@ def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: 
     off = torch.empty(N, dtype=torch.int32, device=dev)
     cnt = torch.empty(N, dtype=torch.int32, device=dev)
     counters = torch.zeros(2, dtype=torch.int32, device=dev)
-    consumed = torch.zeros(1, dtype=torch.int64, device=dev)
+    stats = torch.zeros(2, dtype=torch.int64, device=dev)  # [0] composited (queried), [1] evaluated
+    # the largest K times every ray, or the byte budget (a ray that does not fit waits a round)
+    cap = max(1, min(N * max(k_schedule), round_bytes // MARCH_POINT_BYTES, 2 ** 31 - 1))
+    cap = max(cap, max(k_schedule))
+    out_ray = torch.empty(cap, dtype=torch.int32, device=dev)
+    out_step = torch.empty(cap, dtype=torch.int32, device=dev)
+    out_pts = torch.empty(cap, 3, device=dev)
+    raw = torch.empty(cap, 4, device=dev)
     # unit view directions of every ray (d / |d|), as render_accelerated computes per query
     _, _, vd = sample_stratified(rays, near, far, 1, False, want_pts=False)
     check(L.nerf_march_init(ptr(T), ptr(rgb), ptr(depth), ptr(acc), ptr(nxt), ptr(alive), ptr(exh), N, s),
           "nerf_march_init")
     bb = _bbox_arr(bbox)
-    evaluated, rounds, ki, n_alive = 0, 0, 0, N
+    macro = torch.empty(L.nerf_march_macro_bytes(res), dtype=torch.uint8, device=dev) if use_macro else None
+    if macro is not None:
+        check(L.nerf_march_macro(ptr(g), res, ptr(macro), s), "nerf_march_macro")
+    packer.get(dtype_code(dtype), 0)  # (pack before the rounds)
+    rounds = 0
     while True:
-        K = k_schedule[min(ki, len(k_schedule) - 1)]
-        K = max(1, min(K, round_bytes // (MARCH_POINT_BYTES * max(n_alive, 1)), (2 ** 31 - 1) // max(n_alive, 1)))
-        cap = n_alive * K
-        out_ray = torch.empty(cap, dtype=torch.int32, device=dev)
-        out_step = torch.empty(cap, dtype=torch.int32, device=dev)
-        out_pts = torch.empty(cap, 3, device=dev)
+        # (the gather's int32 reservation counter: alive rays x K < 2^31)
+        K = max(1, min(k_schedule[min(rounds, len(k_schedule) - 1)], cap, (2 ** 31 - 1) // max(N, 1)))
         counters.zero_()
-        check(L.nerf_march_gather(ptr(rays), N, ptr(t_table), n_steps, ptr(g), res, bb, K, int(k_low), float(t_split),
-                                  ptr(T), ptr(rgb),
-                                  ptr(depth), ptr(acc), ptr(nxt), ptr(alive), ptr(exh), ptr(counters), ptr(start),
-                                  ptr(out_ray), ptr(out_step), ptr(out_pts), ptr(off), ptr(cnt), cap, s),
-              "nerf_march_gather")
-        n_pts, n_alive = (int(v) for v in counters.tolist())
-        if n_alive == 0:
-            break
-        rounds += 1
-        raw = torch.empty(0, 4, device=dev)
-        if n_pts > 0:
-            with torch.no_grad():
-                raw = mlp(packer, out_pts[:n_pts], vd, 1, out_ray[:n_pts], dtype)
-            evaluated += n_pts
+        check(L.nerf_march_gather(ptr(rays), N, ptr(t_table), n_steps, ptr(g), res, ptr(macro), bb, K, int(k_low),
+                                  float(t_split),
+                                  ptr(T), ptr(rgb), ptr(depth), ptr(acc), ptr(nxt), ptr(alive), ptr(exh),
+                                  ptr(counters), stats[1:].data_ptr(), ptr(start), ptr(out_ray), ptr(out_step),
+                                  ptr(out_pts), ptr(off), ptr(cnt), cap, s), "nerf_march_gather")
+        with torch.no_grad():
+            mlp_count(packer, out_pts, vd, out_ray, counters, raw, dtype)
         check(L.nerf_march_composite(ptr(raw), ptr(rays), N, ptr(t_table), ptr(off), ptr(cnt), ptr(out_step), ptr(T),
                                      ptr(rgb), ptr(depth), ptr(acc), ptr(nxt), ptr(alive), ptr(exh),
-                                     float(step_size), float(t_thresh), ptr(consumed), s), "nerf_march_composite")
-        ki += 1
+                                     float(step_size), float(t_thresh), stats.data_ptr(), s), "nerf_march_composite")
+        rounds += 1
+        if rounds % sync_every == 0 and int(counters[1]) == 0:
+            break
     check(L.nerf_march_finish(ptr(rgb), ptr(acc), N, int(bool(white_bkgd)), s), "nerf_march_finish")
-    return {"rgb_map_f": rgb, "depth_map_f": depth, "acc_map_f": acc, "n_queried": int(consumed.item()),
-            "n_evaluated": evaluated, "rounds": rounds}
+    st = stats.tolist()
+    return {"rgb_map_f": rgb, "depth_map_f": depth, "acc_map_f": acc, "n_queried": int(st[0]),
+            "n_evaluated": int(st[1]), "rounds": rounds}
 
 
 # --------------------------------------------------------------------------------------

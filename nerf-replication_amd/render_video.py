@@ -37,12 +37,32 @@ def _camera():
         return H, W, focal_for(int(cfg.test_dataset.W)) * r
 
 
+def video_poses(n, device=None):
+    """The reference's turntable: pose_spherical(angle, -30, 4) for angle in linspace(-180, 180,
+    n + 1)[:-1] (render_video.py:46-49)."""
+    from src.utils.camera import pose_spherical
+    return torch.stack([pose_spherical(float(a), -30.0, 4.0) for a in np.linspace(-180, 180, n + 1)[:-1]]).to(device)
+
+
+def render_frame(renderer, pose, H, W, focal, near, far, pix=None):
+    """One frame (render_video.py:53-64): the camera's rays (nerf_raygen), Renderer.render (split
+    over the ranks under torchrun), rgb_map_f (else rgb_map_c) -> (float [H,W,3], uint8 [H,W,3]
+    = clip(rgb, 0, 1) * 255 truncated, as the reference's numpy cast), both on the device."""
+    from nerf_amd import ops
+    from src.utils.dist_render import render_distributed
+    if pix is None:
+        pix = torch.arange(H * W, device=pose.device)
+    with torch.no_grad():
+        rays, _, _ = ops.raygen(pose.reshape(1, 4, 4), H, W, focal, pix=pix)
+        out = render_distributed(renderer, {"rays": rays, "near": near, "far": far}, keys=("rgb_map_f", "rgb_map_c"))
+    rgb = out.get("rgb_map_f", out["rgb_map_c"]).reshape(H, W, 3)
+    return rgb, rgb.clamp(0, 1).mul(255).to(torch.uint8)
+
+
 def render_360_video(num_frames=None, write=True):
     from nerf_amd import ops
     from src.models import make_network
     from src.models.nerf.renderer.make_renderer import make_renderer
-    from src.utils.camera import pose_spherical
-    from src.utils.dist_render import render_distributed
     from src.utils.net_utils import load_network
 
     rank = 0
@@ -59,7 +79,7 @@ def render_360_video(num_frames=None, write=True):
     network.to(device).eval()
     renderer = make_renderer(cfg, network)
     n = int(num_frames or cfg.get("video_frames", 240))
-    poses = torch.stack([pose_spherical(float(a), -30.0, 4.0) for a in np.linspace(-180, 180, n + 1)[:-1]]).to(device)
+    poses = video_poses(n, device)
     H, W, focal = _camera()
     near = ops.device_scalar(float(cfg.task_arg.near), device)
     far = ops.device_scalar(float(cfg.task_arg.far), device)
@@ -69,14 +89,10 @@ def render_360_video(num_frames=None, write=True):
         os.makedirs(out_dir, exist_ok=True)
     frames, t0 = [], time.time()
     for i in range(n):
-        with torch.no_grad():
-            rays, _, _ = ops.raygen(poses[i:i + 1], H, W, focal, pix=pix)
-            out = render_distributed(renderer, {"rays": rays, "near": near, "far": far},
-                                     keys=("rgb_map_f", "rgb_map_c"))
+        _, img = render_frame(renderer, poses[i], H, W, focal, near, far, pix)
         if rank != 0:
             continue
-        img = out.get("rgb_map_f", out["rgb_map_c"]).reshape(H, W, 3).clamp(0, 1).mul(255).to(torch.uint8).cpu()
-        frames.append(img.numpy())
+        frames.append(img.cpu().numpy())
         if write:
             from PIL import Image
             Image.fromarray(frames[-1]).save(os.path.join(out_dir, f"frame_{i:03d}.png"))

@@ -8,15 +8,18 @@ K2 = 0.03, sample covariance N/(N-1), border of 3 px cropped before the mean, me
 channels).  Parity of this restatement with scikit-image is unpinned here (no skimage
 to compare against).  PNG dumps use PIL instead of cv2.
 
-When the rendered image is on the GPU the metrics run there (``nerf_image_metrics``,
-csrc/metrics.hip: exact integer window sums, fp64 SSIM formula); the numpy functions
-below are the same definitions on the host (used for host images and as the GPU
-kernel's test reference).
+When the rendered image is on the GPU (run.py --type evaluate, Trainer.val) the metrics
+run there (``nerf_image_metrics``, csrc/metrics.hip: exact integer window sums, fp64 SSIM
+formula), and the PNG dump (save_result, the reference's default) is written from the uint8
+images converted on the device: one 1.9 MB copy per 800x800 view instead of the float image
+and a host SSIM.  The numpy functions below are the same definitions on the host (used for
+host images and as the GPU kernel's test reference).
 """
 import json
 import os
 
 import numpy as np
+import torch
 from scipy.ndimage import uniform_filter
 
 from src.config import cfg
@@ -54,13 +57,17 @@ class Evaluator:
     def psnr_metric(self, img_pred, img_gt):
         return psnr_metric(img_pred, img_gt)
 
+    def save_pngs(self, pred_u8, gt_u8, id):
+        """view{id}_pred.png / _gt.png under result_dir/images (nerf.py:29-38 of the reference)."""
+        from PIL import Image
+        d = os.path.join(cfg.result_dir, "images")
+        os.makedirs(d, exist_ok=True)
+        Image.fromarray(pred_u8).save(f"{d}/view{id:03d}_pred.png")
+        Image.fromarray(gt_u8).save(f"{d}/view{id:03d}_gt.png")
+
     def ssim_metric(self, img_pred, img_gt, batch, id, num_imgs):
         if self.save_images:
-            from PIL import Image
-            d = os.path.join(cfg.result_dir, "images")
-            os.makedirs(d, exist_ok=True)
-            Image.fromarray(np.clip(img_pred * 255, 0, 255).astype(np.uint8)).save(f"{d}/view{id:03d}_pred.png")
-            Image.fromarray(img_gt).save(f"{d}/view{id:03d}_gt.png")
+            self.save_pngs(np.clip(img_pred * 255, 0, 255).astype(np.uint8), img_gt, id)
         return ssim_metric_uint8((img_pred * 255).astype(np.uint8), img_gt)
 
     def evaluate(self, output, batch):
@@ -68,9 +75,13 @@ class Evaluator:
         H, W = int(batch["H"].reshape(-1)[0]), int(batch["W"].reshape(-1)[0])
         pred_t = output["rgb_map_f"].detach().float()
         gt_t = batch["rgbs"].detach().float()
-        if pred_t.is_cuda and gt_t.is_cuda and not self.save_images:
+        if pred_t.is_cuda and gt_t.is_cuda:
             from nerf_amd import ops
-            psnr, ssim = ops.image_metrics(pred_t.reshape(H, W, 3), gt_t.reshape(H, W, 3))
+            pred_t, gt_t = pred_t.reshape(H, W, 3), gt_t.reshape(H, W, 3)
+            psnr, ssim = ops.image_metrics(pred_t, gt_t)
+            if self.save_images:
+                self.save_pngs((pred_t * 255).clamp(0, 255).to(torch.uint8).cpu().numpy(),
+                               (gt_t * 255).to(torch.uint8).cpu().numpy(), i)
             self.psnr.append(psnr)
             self.ssim.append(ssim)
             return {"psnr": psnr, "ssim": ssim}

@@ -15,7 +15,8 @@ hierarchical render is pinned at:
     on 1 of 64 rays, 16 silhouette pixels of the 100x100 view up to 1.7e-3, gradients up to
     1.1e-3 (the near-converged trained net's gradients are sums of cancelling terms);
   * bf16 MLP (opt-in): rgb / depth / acc within 2e-3 absolute on >= 95 % of the values and
-    within 3e-2 on all of them, PSNR within 0.05 dB.  Rounding the trained weights OR the
+    within 3e-2 on all of them, PSNR within 0.05 dB; gradients as the emulation of its rounding
+    predicts (GRAD_REL / BF16_GRAD_L2 below).  Rounding the trained weights OR the
     activations to bf16 alone already moves rgb by up to 4.6e-3 / 5.3e-3 on these rays
     (CPU emulation), so 2e-3 everywhere is out of reach of any bf16 MLP; no ray
     is excluded and the depth tolerance is not scaled;
@@ -36,7 +37,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 KEYS = ["rgb_map_c", "depth_map_c", "acc_map_c", "rgb_map_f", "depth_map_f", "acc_map_f"]
 TOL = {"fp32": 1e-4, "bf16x3": 1e-4, "bf16": 2e-3}
 MAXERR = {"fp32": 1e-4, "bf16x3": 2e-3, "bf16": 3e-2}  # bound on every value
-GRAD_REL = {"fp32": 1e-4, "bf16x3": 2e-3}
+# bf16: the trained net's gradient entries are sums of cancelling per-sample terms, and rounding
+# every activation to 8 bits moves them by up to 74 % (64 rays) / 31 % (4096 rays) of the tensor's
+# largest entry, 0.37 / 0.089 in relative L2 over the sampled entries -- exactly what the CPU
+# emulation of the bf16 kernels' rounding predicts (tools/precision_rank.py b:b: 0.737 / 0.310,
+# 0.365 / 0.089), so the kernels are pinned to their rounding model (test_gpu_kernels.py
+# BF16_EMU_TOL) and these bounds only hold the end-to-end gradient to what that model gives
+GRAD_REL = {"fp32": 1e-4, "bf16x3": 2e-3, "bf16": 1.0}
+BF16_GRAD_L2 = {"grad64": 0.5, "grad4096": 0.15}
 
 
 @pytest.fixture(scope="module")
@@ -129,18 +137,32 @@ def test_render_perturb1_injected(g2, cuda, stack, dtype):
 
 
 def _grad_check(net, g2, tag, rel=1e-4):
+    """Every sampled entry within rel x its tensor's largest (or 1e-8), every tensor norm within rel;
+    returns the sampled entries' relative L2 error (each tensor scaled by its largest entry)."""
     params = dict(net.named_parameters())
+    worst, worst_norm = (0.0, ""), (-1.0, "")
+    num = den = 0.0
     for i, name in enumerate(g2[f"{tag}_names"]):
         g = params[str(name)].grad.reshape(-1).double().cpu()
         norm = float(torch.linalg.vector_norm(g))
-        np.testing.assert_allclose(norm, g2[f"{tag}_norms"][i], rtol=rel, atol=1e-8, err_msg=str(name))
+        ref_norm = g2[f"{tag}_norms"][i]
+        np.testing.assert_allclose(norm, ref_norm, rtol=rel, atol=1e-8, err_msg=str(name))
+        worst_norm = max(worst_norm, (abs(norm - ref_norm) / ref_norm, str(name)))
         sel = g[torch.from_numpy(g2[f"{tag}_sel_idx"][i])].numpy()
         scale = float(g2[f"{tag}_absmax"][i]) + 1e-30
         err = float(np.abs(sel - g2[f"{tag}_sel_val"][i]).max())
-        assert err < rel * scale or err < 1e-8, (str(name), err / scale)
+        num += float((((sel - g2[f"{tag}_sel_val"][i]) / scale) ** 2).sum())
+        den += float(((g2[f"{tag}_sel_val"][i] / scale) ** 2).sum())
+        if err >= 1e-8:
+            worst = max(worst, (err / scale, str(name)))
+    l2 = float(np.sqrt(num / den))
+    print(f"\n{tag}: largest entry error {worst[0]:.2e} of the tensor's largest ({worst[1]}), "
+          f"norm {worst_norm[0]:.2e} ({worst_norm[1]}), sampled-entry relative L2 {l2:.2e}")
+    assert worst[0] < rel, worst
+    return l2
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16"])
 @pytest.mark.parametrize("tag,n", [("grad64", 64), ("grad4096", 4096)])
 def test_loss_gradients_fp32(g2, cuda, stack, tag, n, dtype):
     """MSE(c) + MSE(f) and its gradient w.r.t. all 48 tensors through the autograd path
@@ -154,8 +176,11 @@ def test_loss_gradients_fp32(g2, cuda, stack, tag, n, dtype):
     batch["rgbs"] = torch.from_numpy(g2[f"{tag}_gt"]).to(cuda)
     _, loss, stats = wrapper(batch)
     loss.backward()
-    np.testing.assert_allclose([float(stats["loss_c"]), float(stats["loss_f"])], g2[f"{tag}_loss"], rtol=1e-5)
-    _grad_check(net, g2, tag, GRAD_REL[dtype])
+    np.testing.assert_allclose([float(stats["loss_c"]), float(stats["loss_f"])], g2[f"{tag}_loss"],
+                               rtol=1e-5 if dtype != "bf16" else 2e-2)
+    l2 = _grad_check(net, g2, tag, GRAD_REL[dtype])
+    if dtype == "bf16":
+        assert l2 < BF16_GRAD_L2[tag], l2
     net.zero_grad()
 
 
@@ -281,3 +306,64 @@ def test_occupancy_grid_entry_point(g2, cuda, stack, tmp_path):
     assert grid.dtype == torch.bool and tuple(grid.shape) == (128, 128, 128)
     diff = torch.nonzero((grid != _golden_grid(g2)).reshape(-1)).reshape(-1).numpy()
     assert set(diff.tolist()) <= set(g2["bake128_near_threshold_voxels"].tolist()), diff[:20]
+
+
+@pytest.fixture(scope="module")
+def g3():
+    return np.load(os.path.join(HERE, "golden", "golden_v3.npz"), allow_pickle=False)
+
+
+def test_render_video_frames_match_reference(g3, cuda, stack, tmp_path):
+    """render_video.py (reference render_video.py:21-70) against frames the REFERENCE rendered
+    (tests/golden/make_golden_v3.py: the trained weights, its turntable poses 0/37/120/201 of 240,
+    the test camera at input_ratio 0.05 = 40x40, perturb 0): the poses bit-exact; the camera rays
+    (nerf_raygen) against the reference's get_rays -- origins exact, directions within 2e-7 (its
+    CPU matmul vs separately rounded products); rendering the REFERENCE's rays, every rgb_map_f
+    value within 1e-4 (fp32); the frame from our own rays (the render_video path) within 1e-4 on
+    >= 99.5 % of the values and 1e-3 on all (a silhouette pixel moves with a 1e-7 direction
+    change) and the uint8 frames within one level; then the entry point itself (``python
+    render_video.py --cfg_file configs/nerf/lego.yaml ...``, latest.pth from trained_model_dir)
+    writes PNG frames identical to the in-process ones."""
+    import subprocess
+    import sys
+    from PIL import Image
+    from nerf_amd import ops
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "nerf-replication_amd"))
+    import render_video
+    cfg, net, r = stack
+    net.mlp_dtype = "fp32"
+    H, W, focal = int(g3["H"]), int(g3["W"]), float(g3["focal"])
+    poses = render_video.video_poses(int(g3["n_frames"]), cuda)
+    near, far = ops.device_scalar(2.0, cuda), ops.device_scalar(6.0, cuda)
+    ours = {}
+    for k in g3["frames"].tolist():
+        np.testing.assert_array_equal(poses[k].cpu().numpy(), g3[f"video_pose_{k}"])
+        ref_rays = torch.from_numpy(g3[f"video_rays_{k}"]).to(cuda)
+        rays, _, _ = ops.raygen(poses[k].reshape(1, 4, 4), H, W, focal, pix=torch.arange(H * W, device=cuda))
+        np.testing.assert_array_equal(rays[:, :3].cpu().numpy(), g3[f"video_rays_{k}"][:, :3])
+        np.testing.assert_allclose(rays[:, 3:].cpu().numpy(), g3[f"video_rays_{k}"][:, 3:], rtol=0, atol=2e-7)
+        with torch.no_grad():
+            on_ref = r.render({"rays": ref_rays, "near": near, "far": far})["rgb_map_f"]
+        np.testing.assert_allclose(on_ref.cpu().numpy(), g3[f"video_rgb_{k}"], rtol=0, atol=1e-4)
+        rgb, img = render_video.render_frame(r, poses[k], H, W, focal, near, far)
+        err = np.abs(rgb.reshape(-1, 3).cpu().numpy() - g3[f"video_rgb_{k}"])
+        assert (err <= 1e-4).mean() >= 0.995 and err.max() <= 1e-3, (k, float((err <= 1e-4).mean()), float(err.max()))
+        d = np.abs(img.cpu().numpy().astype(int) - g3[f"video_frame_{k}"].astype(int))
+        assert d.max() <= 1 and (d == 0).mean() >= 0.99, (k, d.max(), (d == 0).mean())
+        ours[k] = img.cpu().numpy()
+    mdir = tmp_path / "model" / "nerf_replication" / "lego" / "nerf"
+    mdir.mkdir(parents=True)
+    torch.save({"net": {k: v.cpu() for k, v in net.state_dict().items()}, "epoch": 9}, mdir / "latest.pth")
+    root = os.path.dirname(HERE)
+    env = {k: v for k, v in os.environ.items() if k != "NERF_AMD_NO_ARGV"}
+    res = subprocess.run([sys.executable, os.path.join(root, "nerf-replication_amd", "render_video.py"),
+                          "--cfg_file", "configs/nerf/lego.yaml", "trained_model_dir", str(tmp_path / "model"),
+                          "result_dir", str(tmp_path / "result"), "test_dataset.input_ratio", "0.05",
+                          "task_arg.perturb", "0", "video_frames", str(int(g3["n_frames"]))],
+                         cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
+    frames_dir = next((tmp_path / "result").rglob("video_frames"))
+    assert len(list(frames_dir.glob("frame_*.png"))) == int(g3["n_frames"])
+    for k, img in ours.items():
+        png = np.asarray(Image.open(frames_dir / f"frame_{k:03d}.png"))
+        np.testing.assert_array_equal(png, img)

@@ -13,10 +13,11 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ["fwd_kernel<nerf::mlp::PBF16, true, false>", "fwd_kernel<nerf::mlp::PBF16, false, false>",
-           "fwd_kernel<nerf::mlp::PBF16, false, true>", "fwd_kernel<nerf::mlp::PF32, true, false>",
-           "fwd_kernel<nerf::mlp::PF32, false, false>", "dx_kernel<nerf::mlp::PBF16>", "dx_kernel<nerf::mlp::PF32>",
-           "dw_kernel<nerf::mlp::PBF16>", "dw_kernel<nerf::mlp::PF32>"]
+KERNELS = ["fwd_kernel<nerf::mlp::PBF16, true, false, false>", "fwd_kernel<nerf::mlp::PBF16, false, false, false>",
+           "fwd_kernel<nerf::mlp::PBF16, false, true, false>", "fwd_kernel<nerf::mlp::PF32, true, false, false>",
+           "fwd_kernel<nerf::mlp::PF32, false, false, false>", "dx_kernel<nerf::mlp::PBF16>", "dx_kernel<nerf::mlp::PF32>",
+           "dw_kernel<nerf::mlp::PBF16>", "dw_kernel<nerf::mlp::PF32>",
+           "fwd_kernel<nerf::mlp::PF32, false, false, true>", "fwd_kernel<nerf::mlp::PBF16, false, false, true>"]
 
 
 def build_asm(tmp, kernels=None):
@@ -68,7 +69,10 @@ def check(asm):
             if m and i + 1 < len(lines) and "s_barrier" in lines[i + 1] and since is not None:
                 waits += 1
                 unsafe += int(m.group(1)) > since
-        straight = "dw_kernel" in name or "dw_reduce" in name or not loops
+        # the persistent inference forward (PERSIST = true) loops over its sample blocks: the block
+        # loop (+ its guard) is its only backward branch
+        persist = re.search(r"fwd_kernel\w*?ELb0ELb0ELb1E", name) is not None
+        straight = "dw_kernel" in name or "dw_reduce" in name or not loops or (persist and len(loops) <= 2)
         ok = straight and not unsafe
         bad += not ok
         print(f"{'ok ' if ok else 'BAD'} {name[:70]:70s} loops={len(loops)} counted_waits={waits} unsafe={unsafe}")

@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--lib", default=None, help="alternative build of libnerf_amd.so")
-    ap.add_argument("--schedule", default=None, help="time only this schedule")
+    ap.add_argument("--schedule", default=None, help="time only these schedules (comma-separated names)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     from nerf_amd import _lib
@@ -57,11 +57,13 @@ def main():
         variants = [(n, sc, 1024, 2.0) for n, sc in SCHEDULES.items()]  # t_split 2: k_low never used
         variants += [(f"{n}_klow{kl}_t{tsp}", SCHEDULES[n], kl, tsp) for n in ("12x2", "16x2")
                      for kl in (2, 4, 8) for tsp in (0.5, 0.9)]
-        for name, sched, kl, tsp in variants:
-            if args.schedule and name != args.schedule:
+        variants = [(n + (f"_sync{se}" if se != 4 else ""), sc, kl, tsp, se) for n, sc, kl, tsp in variants
+                    for se in (4, 8)]
+        for name, sched, kl, tsp, se in variants:
+            if args.schedule and name not in args.schedule.split(","):
                 continue
             run = lambda: ops.march(net.model_fine.packer(), rays, 2.0, 6.0, grid, dtype=args.dtype,  # noqa: E731
-                                    k_schedule=sched, k_low=kl, t_split=tsp)
+                                    k_schedule=sched, k_low=kl, t_split=tsp, sync_every=se)
             run()
             torch.cuda.synchronize()
             ts = []

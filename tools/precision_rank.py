@@ -131,10 +131,13 @@ def grad_errors(fcfg, bcfg, g2, state, tag="grad64"):
     finally:
         O.mlp = orig
     worst, wn, worst_norm = 0.0, None, 0.0
+    num = den = 0.0
     for i, name in enumerate(g2[f"{tag}_names"]):
         g = params[str(name)].grad.reshape(-1).double()
         sel = g[torch.from_numpy(g2[f"{tag}_sel_idx"][i])].numpy()
         scale = float(g2[f"{tag}_absmax"][i]) + 1e-30
+        num += float((((sel - g2[f"{tag}_sel_val"][i]) / scale) ** 2).sum())
+        den += float(((g2[f"{tag}_sel_val"][i] / scale) ** 2).sum())
         e = float(np.abs(sel - g2[f"{tag}_sel_val"][i]).max())
         if e < 1e-8:
             e = 0.0
@@ -142,6 +145,7 @@ def grad_errors(fcfg, bcfg, g2, state, tag="grad64"):
             worst, wn = e / scale, str(name)
         nr = abs(float(torch.linalg.vector_norm(g)) - g2[f"{tag}_norms"][i]) / (g2[f"{tag}_norms"][i] + 1e-30)
         worst_norm = max(worst_norm, nr)
+    print(f"  sampled-entry relative L2 error (each tensor over its largest entry): {np.sqrt(num / den):.2e}")
     return worst, wn, worst_norm
 
 
