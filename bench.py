@@ -474,7 +474,7 @@ def cpu_baseline(n_rays):
                       f"mean of {reps} after 1 warm-up, oracle restatement on torch CPU"}
 
 
-def eager_gpu_baseline(device, n_rays, dtype, reps=3):
+def eager_gpu_baseline(device, n_rays, dtype, reps=11):
     """Baseline leg: the reference's per-step op graph (the oracle restatement of
     volume_renderer.render + network.Network + MSE + clip_grad_value_(40) + Adam with one group
     per tensor) run eagerly by PyTorch-ROCm on this GPU -- the "reference per-step PyTorch-ROCm
@@ -496,15 +496,18 @@ def eager_gpu_baseline(device, n_rays, dtype, reps=3):
         opt.step()
 
     step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    times = []
     for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         step()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / reps
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    dt = times[len(times) // 2]
     return {"value": round(n_rays / dt, 1), "unit": "rays/s", "kind": "pytorch_rocm_eager", "dtype": dtype,
-            "ms_per_step": round(dt * 1e3, 2),
-            "sample": f"{n_rays}-ray full train step (perturb 1, clip 40 + torch.optim.Adam), mean of {reps} "
+            "ms_per_step": round(dt * 1e3, 2), "ms_per_step_min_max": [round(times[0] * 1e3, 2), round(times[-1] * 1e3, 2)],
+            "sample": f"{n_rays}-ray full train step (perturb 1, clip 40 + torch.optim.Adam), median of {reps} "
                       f"after 1 warm-up, reference op graph (oracle restatement) on PyTorch-ROCm {torch.__version__}"}
 
 

@@ -92,6 +92,33 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// torch.sum(x, -1) of one contiguous fp32 row on the CPU, bit for bit, for n <= 64 values held
+// one per lane (x_i on lane i, any value beyond n).  sample_pdf normalises by this sum
+// (volume_renderer.py:91-92) and a trained net's fine samples move by an ulp with it (an
+// 800x800 silhouette pixel: 3.4e-5 of rgb per ulp), so the order is ATen's, not a tree:
+// vectorized_inner_sum (SumKernel.cpp) over 8-lane float vectors v_j = x[8j, 8j+8), j < nv =
+// n/8: row_sum's ilp-4 partials p_k = sum_r v_{4r+k} (r < nv/4, multi_row_sum below its first
+// 16-row level), the leftover vectors added to p_0, then p_0 + p_1 + p_2 + p_3; the scalar tail
+// x[8nv, n) summed from 0, then the 8 vector lanes added in order.  Matches torch 2.10 CPU on
+// every one of 20,000 random 62-value rows (tree sum: 52 %, fp64: 57 %).
+__device__ __forceinline__ float torch_row_sum(float x, int n) {
+  const int j = lane_id() & 7;
+  const int nv = n >> 3, nilp = nv >> 2;
+  float p[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    p[k] = 0.f;
+    for (int r = 0; r < nilp; ++r) p[k] = fadd(p[k], __shfl(x, (4 * r + k) * 8 + j, 64));
+  }
+  for (int i = 4 * nilp; i < nv; ++i) p[0] = fadd(p[0], __shfl(x, 8 * i + j, 64));
+  const float p0 = fadd(fadd(fadd(p[0], p[1]), p[2]), p[3]);
+  float s = 0.f;
+  for (int k = 8 * nv; k < n; ++k) s = fadd(s, __shfl(x, k, 64));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s = fadd(s, __shfl(p0, k, 64));
+  return s;
+}
+
 // inclusive product scan across the wave, in double (torch CPU cumprod accumulates in
 // double; the exact sum/product of <=256 fp32 terms rarely needs more than 53 bits).
 __device__ __forceinline__ double wave_scan_mul(double v) {

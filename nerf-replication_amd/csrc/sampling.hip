@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(256) sample_pdf_kernel(PdfArgs a) {
   const float zn = __shfl(zc, l + 1 < 64 ? l + 1 : 63, 64);
   const float bin = l < nb ? fmul(0.5f, fadd(zn, zc)) : 0.f;  // .5 * (z[1:] + z[:-1])
   const float w = l < nw ? fadd(a.weights[r * a.Sc + l + 1], 1e-5f) : 0.f;
-  const float wsum = wave_sum(w);
+  const float wsum = torch_row_sum(w, nw);  // the CPU torch.sum's order (common.h)
   const float pdf = l < nw ? fdiv(w, wsum) : 0.f;
   // cdf[0] = 0, cdf[k] = fp32(sum_{j<k} pdf_j) accumulated in double (torch CPU cumsum)
   const double incl = wave_scan_add((double)pdf);
@@ -303,7 +303,7 @@ __global__ void __launch_bounds__(256) sample_pdf_bins_kernel(PdfBinsArgs a) {
   const int nw = a.nb - 1;
   const float bin = l < a.nb ? a.bins[r * a.nb + l] : 0.f;
   const float w = l < nw ? fadd(a.weights[r * nw + l], 1e-5f) : 0.f;
-  const float wsum = wave_sum(w);
+  const float wsum = torch_row_sum(w, nw);
   const float pdf = l < nw ? fdiv(w, wsum) : 0.f;
   const double incl = wave_scan_add((double)pdf);
   const double excl = __shfl_up(incl, 1, 64);
