@@ -184,6 +184,19 @@ def mlp_roofline(k, n, ms, units, dtype):
             "avg_launch_ms": round(avg_ms, 4)}
 
 
+def hbm_roofline(k, n, ms, dtype):
+    """The same launch against HBM: PMC bytes per launch (the newest committed traffic summary
+    for this dtype, profiles/r*/traffic_*.json) / its mean HIP-event duration, against 8 TB/s.
+    The bf16 training kernels move their stored tiles at 4.6-5.7 TB/s (the ~6.3 TB/s a copy
+    reaches, MI355X_MICROARCH.md): HBM, not the MFMA, bounds them."""
+    traffic, src = pmc_traffic(k, dtype)
+    if traffic is None:
+        return None
+    ach = traffic / (ms / n * 1e-3) / 1e9
+    return {"bound": "hbm", "traffic": traffic, "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic_source": src}
+
+
 def measure_training(args, world, rank, device, dtype):
     """Warmup + exactly args.steps timed steps (barrier + synchronize on both sides, max over
     ranks).  Returns (rays/s, ms/step, roofline, per-kernel table, train-size stream kernels,
@@ -223,8 +236,8 @@ def measure_training(args, world, rank, device, dtype):
                     traffic_unit="HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)", traffic_source=traffic_src,
                     store_bytes_per_launch=store_bytes, mlp_io_bytes_per_launch=io_bytes,
                     traffic_vs_mlp_io=None if traffic is None else round(traffic / io_bytes, 1))
-    kt = {k: {"launches": n, "avg_ms": round(m / n, 4), "roofline": mlp_roofline(k, n, m, u, dtype)}
-          for k, (n, m, u) in ktimes.items()}
+    kt = {k: {"launches": n, "avg_ms": round(m / n, 4), "roofline": mlp_roofline(k, n, m, u, dtype),
+              "hbm": hbm_roofline(k, n, m, dtype)} for k, (n, m, u) in ktimes.items()}
     return value, elapsed / args.steps * 1e3, roofline, kt, train_stream, (cfg, net, ds)
 
 

@@ -57,8 +57,19 @@ class Evaluator:
     def psnr_metric(self, img_pred, img_gt):
         return psnr_metric(img_pred, img_gt)
 
+    @staticmethod
+    def png_pixels(img_pred, img_gt_u8):
+        """The pixel values the reference's cv2.imwrite calls store (nerf.py:31-38): the float
+        prediction x 255 converted by OpenCV's saturate_cast (round half to even, clamp to
+        [0, 255]); the ground truth is already uint8 there, and its ``* 255`` stays uint8 and
+        wraps modulo 256 (NumPy keeps the array's dtype for a Python int operand), so the
+        reference's gt PNG holds (255 g) mod 256 -- reproduced as written."""
+        pred = np.clip(np.rint(img_pred.astype(np.float32) * np.float32(255)), 0, 255).astype(np.uint8)
+        return pred, (img_gt_u8 * 255).astype(np.uint8)
+
     def save_pngs(self, pred_u8, gt_u8, id):
-        """view{id}_pred.png / _gt.png under result_dir/images (nerf.py:29-38 of the reference)."""
+        """view{id}_pred.png / _gt.png under result_dir/images (nerf.py:29-38 of the reference);
+        pixel values as png_pixels gives them."""
         from PIL import Image
         d = os.path.join(cfg.result_dir, "images")
         os.makedirs(d, exist_ok=True)
@@ -67,7 +78,7 @@ class Evaluator:
 
     def ssim_metric(self, img_pred, img_gt, batch, id, num_imgs):
         if self.save_images:
-            self.save_pngs(np.clip(img_pred * 255, 0, 255).astype(np.uint8), img_gt, id)
+            self.save_pngs(*self.png_pixels(img_pred, img_gt), id)
         return ssim_metric_uint8((img_pred * 255).astype(np.uint8), img_gt)
 
     def evaluate(self, output, batch):
@@ -79,9 +90,10 @@ class Evaluator:
             from nerf_amd import ops
             pred_t, gt_t = pred_t.reshape(H, W, 3), gt_t.reshape(H, W, 3)
             psnr, ssim = ops.image_metrics(pred_t, gt_t)
-            if self.save_images:
-                self.save_pngs((pred_t * 255).clamp(0, 255).to(torch.uint8).cpu().numpy(),
-                               (gt_t * 255).to(torch.uint8).cpu().numpy(), i)
+            if self.save_images:  # png_pixels on the device: one uint8 copy per image
+                pred_png = torch.round(pred_t * 255).clamp(0, 255).to(torch.uint8)
+                gt_png = ((gt_t * 255).to(torch.uint8).to(torch.int32) * 255 % 256).to(torch.uint8)
+                self.save_pngs(pred_png.cpu().numpy(), gt_png.cpu().numpy(), i)
             self.psnr.append(psnr)
             self.ssim.append(ssim)
             return {"psnr": psnr, "ssim": ssim}

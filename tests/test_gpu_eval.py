@@ -46,6 +46,14 @@ def test_evaluator_default_path_on_gpu(cuda, tmp_path):
         assert abs(got["ssim"] - host["ssim"]) < 1e-9, (got, host)
         for name in ("view003_pred.png", "view003_gt.png"):
             np.testing.assert_array_equal(np.asarray(Image.open(gdir / name)), np.asarray(Image.open(hdir / name)))
+        # the reference's cv2.imwrite values: saturate_cast (round half to even) of pred x 255,
+        # and its uint8 gt x 255 wrapped modulo 256
+        p32 = pred.reshape(H, W, 3).numpy()
+        np.testing.assert_array_equal(np.asarray(Image.open(gdir / "view003_pred.png")),
+                                      np.clip(np.rint(p32 * np.float32(255)), 0, 255).astype(np.uint8))
+        g8 = (gt.reshape(H, W, 3).numpy() * 255).astype(np.uint8)
+        np.testing.assert_array_equal(np.asarray(Image.open(gdir / "view003_gt.png")),
+                                      ((g8.astype(np.int64) * 255) % 256).astype(np.uint8))
         cfg.result_dir = str(tmp_path / "gpu")
         s = e.summarize()
         with open(tmp_path / "gpu" / "summary.json") as f:
