@@ -583,6 +583,15 @@ def main():
             "cpu_baseline": cpu,
         }
         line.update({k: v for k, v in head.items() if k not in line and k not in ("value", "dtype")})
+        # north_star "800x800 test view rendered in < 0.5 s on the node", per MLP dtype: the
+        # hierarchical render (volume_renderer.render, 64 + 128 samples) and render_accelerated
+        # (the grid march, the reference's own fast path once occupancy_grid.pt exists) of the
+        # trained fixture's held-out view, both split over the N GPUs of this run
+        line["render_800x800_s"] = {
+            d: None if lines[d]["occupancy_grid"] is None else {
+                "hierarchical": lines[d]["occupancy_grid"]["trained"]["hierarchical_render_s"],
+                "accelerated": lines[d]["occupancy_grid"]["trained"]["march_s_per_frame"], "gpus": world}
+            for d in lines}
         line["baseline"] = head["baseline"]
         for d in others:
             line[f"{d}_line"] = dict(lines[d], label=f"opt-in {d} MLP (same workload)", metric=METRIC, unit="rays/s")

@@ -325,6 +325,128 @@ __global__ void march_emit_kernel(MarchEmitArgs e) {
   }
 }
 
+// One-pass gather + emit (the default since round 3).  The two-pass form above walks every
+// ray twice: once to count its points (the wave's reservation needs every lane's count
+// first), once more, with every grid lookup again, to write them (the bf16 trained-net frame:
+// 1.4 of 17 ms in emit).  Here the counting walk records where the points are -- as runs of
+// consecutive occupied steps, up to MARCH_RUNS per lane in LDS (a run of an occupied cell is
+// ~4.7 steps) plus the open one in registers -- and the points are written from the runs
+// after the reservation, with no lookups.  A lane whose runs do not fit remembers where its
+// first unrecorded run starts and walks again from there for the rest (the same walk: the
+// same steps).  Outputs, counters and overflow handling are those of gather + emit.
+constexpr int MARCH_RUNS = 16;
+constexpr int MARCH_WAVES = 4;  // 256-thread blocks
+__device__ __forceinline__ void march_put(const MarchGatherArgs& a, int64_t r, const float* ray, int64_t at, int s) {
+  float p[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = fadd(ray[k], fmul(a.t_table[s], ray[3 + k]));  // = march_occupied's p
+  a.out_ray[at] = (int32_t)r;
+  a.out_step[at] = s;
+  a.out_pts[at * 3 + 0] = p[0];
+  a.out_pts[at * 3 + 1] = p[1];
+  a.out_pts[at * 3 + 2] = p[2];
+}
+
+__global__ void __launch_bounds__(256) march_gather_emit_kernel(MarchGatherArgs a) {
+  __shared__ uint32_t runs[MARCH_WAVES][MARCH_RUNS][64];  // (start << 16) | length, lane-minor
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int w = threadIdx.x >> 6, l = lane_id();
+  const bool in = r < a.N;
+  const bool live = in && a.st.alive[r];
+  int cnt = 0, s = live ? a.st.next_step[r] : 0;
+  const float* ray = a.rays + (in ? r : 0) * 6;
+  int nrun = 0, cur_start = 0, cur_len = 0;  // recorded runs; the open run
+  int ovf_step = -1;                           // first unrecorded run's step
+  if (live) {
+    const int k = a.st.T[r] < a.t_split ? (a.k_low < a.K ? a.k_low : a.K) : a.K;
+    float p[3];
+    int cell[3];
+    while (s < a.n_steps && cnt < k) {
+      if (march_occupied(a, ray, a.t_table[s], p, cell)) {
+        if (ovf_step < 0) {
+          if (cur_len > 0 && s == cur_start + cur_len && cur_len < 0xFFFF) {
+            ++cur_len;
+          } else {
+            if (cur_len > 0) {
+              if (nrun < MARCH_RUNS) {
+                runs[w][nrun][l] = ((uint32_t)cur_start << 16) | (uint32_t)cur_len;
+                ++nrun;
+              } else {  // out of slots: the open run and everything after it are walked again
+                ovf_step = cur_start;
+              }
+            }
+            if (ovf_step < 0) {
+              cur_start = s;
+              cur_len = 1;
+            }
+          }
+        }
+        ++cnt;
+        ++s;
+      } else {
+        s = march_next_after_empty(a, ray, s, cell);
+      }
+    }
+  }
+  // wave-aggregated reservation (as march_gather_kernel)
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int t = __shfl_up(incl, o, 64);
+    if (l >= o) incl += t;
+  }
+  const int wtotal = __shfl(incl, 63, 64);
+  int base = 0;
+  if (l == 63 && wtotal > 0) {
+    base = atomicAdd(&a.counters[0], wtotal);
+    const int64_t below = a.cap - (int64_t)base;
+    if (a.evaluated && below > 0) atomicAdd(a.evaluated, (unsigned long long)(below < wtotal ? below : wtotal));
+  }
+  base = __shfl(base, 63, 64);
+  const unsigned long long live_mask = __ballot(live);
+  if (l == 0 && live_mask) atomicAdd(&a.counters[1], __popcll(live_mask));
+  if (!in) return;
+  if (!live) {
+    a.ray_cnt[r] = 0;
+    return;
+  }
+  const int pos = base + incl - cnt;
+  const bool overflow = (int64_t)pos + cnt > a.cap;
+  a.ray_off[r] = pos;
+  int nwrite = cnt;
+  if (overflow) {  // out of room: written below cap only, gathered again next round
+    const int64_t room = a.cap - (int64_t)pos;
+    nwrite = (int)(room <= 0 ? 0 : room < cnt ? room : cnt);
+    a.ray_cnt[r] = -nwrite;
+  } else {
+    a.ray_cnt[r] = cnt;
+    a.st.exhausted[r] = (s >= a.n_steps) ? 1 : 0;
+    a.st.next_step[r] = s;
+  }
+  // emit: the recorded runs, the open run, then (after a run overflow) the walk again
+  int kk = 0;
+  for (int i = 0; i < nrun && kk < nwrite; ++i) {
+    const uint32_t ru = runs[w][i][l];
+    const int st = (int)(ru >> 16), ln = (int)(ru & 0xFFFF);
+    for (int j = 0; j < ln && kk < nwrite; ++j, ++kk) march_put(a, r, ray, (int64_t)pos + kk, st + j);
+  }
+  if (ovf_step < 0) {
+    for (int j = 0; j < cur_len && kk < nwrite; ++j, ++kk) march_put(a, r, ray, (int64_t)pos + kk, cur_start + j);
+  } else {
+    float p[3];
+    int cell[3];
+    for (int ss = ovf_step; kk < nwrite;) {
+      if (march_occupied(a, ray, a.t_table[ss], p, cell)) {
+        march_put(a, r, ray, (int64_t)pos + kk, ss);
+        ++kk;
+        ++ss;
+      } else {
+        ss = march_next_after_empty(a, ray, ss, cell);
+      }
+    }
+  }
+}
+
 struct MarchCompArgs {
   const float* raw;  // [cap,4]
   const float* rays;
@@ -514,7 +636,8 @@ int nerf_march_init(float* T, float* rgb, float* depth, float* acc, int32_t* nex
 
 // counters[0] = points reserved, counters[1] = rays alive entering this round (zero them first);
 // evaluated (nullable) += the points written, min(points reserved, cap).
-// start_step_scratch: [N] int32 workspace.
+// start_step_scratch: [N] int32 workspace of the two-pass form (gather, then emit walking again),
+// or null: the one-pass form (march_gather_emit_kernel, the default).
 int64_t nerf_march_macro_bytes(int res) {
   if (res <= 1) return -1;
   const int64_t m = (res + MACRO - 1) / MACRO;
@@ -542,6 +665,11 @@ int nerf_march_gather(const float* rays, int64_t N, const float* t_table, int n_
   MarchGatherArgs a{rays, N, t_table, n_steps, grid, res, macro, make_bbox(bbox_host), K, k_low, t_split,
                     {T, rgb, depth, acc, next_step, alive, exhausted},
                     counters, evaluated, out_ray, out_step, out_pts, ray_off, ray_cnt, cap};
+  NERF_REQUIRE(n_steps < 65536, "nerf_march_gather: n_steps must be < 65536 (16-bit run starts)");
+  if (!start_step_scratch) {  // one pass: gather + emit fused (march_gather_emit_kernel)
+    hipLaunchKernelGGL(march_gather_emit_kernel, grid1(N), dim3(256), 0, stream, a);
+    return check_launch("nerf_march_gather");
+  }
   if (hipMemcpyAsync(start_step_scratch, next_step, N * sizeof(int32_t), hipMemcpyDeviceToDevice, stream) !=
       hipSuccess) {
     set_error("nerf_march_gather: hipMemcpyAsync failed");

@@ -496,10 +496,13 @@ def test_grid_index_bit_exact(golden, cuda, ops):
     np.testing.assert_array_equal(idx.cpu().numpy(), golden["grid_idx"])
 
 
-@pytest.mark.parametrize("macro", [True, False])
-@pytest.mark.parametrize("res", [128, 512, 1024])
-@pytest.mark.parametrize("density", [0.02, 0.3, "blob"])
-def test_march_gather_empty_cell_skip_exact(cuda, ops, density, res, macro):
+MARCH_CASES = [(d, r, m, True, False) for d in (0.02, 0.3, "blob") for r in (128, 512, 1024) for m in (True, False)]
+MARCH_CASES += [(d, 128, True, False, False) for d in (0.02, 0.3, "blob")]   # the two-pass form
+MARCH_CASES += [(d, 128, True, p, True) for d in (0.3, "blob") for p in (True, False)]  # buffer overflow
+
+
+@pytest.mark.parametrize("density,res,macro,one_pass,tight", MARCH_CASES)
+def test_march_gather_empty_cell_skip_exact(cuda, ops, density, res, macro, one_pass, tight):
     """The march gather skips the steps that provably stay in an empty cell (grid.hip,
     march_skip_empty).  Against brute force -- the occupancy of EVERY step's point o + t d
     (volume_renderer.py:298-309: clamp, normalise, x127, truncate) -- the one-round gather with
@@ -507,7 +510,11 @@ def test_march_gather_empty_cell_skip_exact(cuda, ops, density, res, macro):
     the box and from inside, axis-aligned direction components (d = 0), sparse and dense grids,
     at the config's res 128 and at 512 / 1024 (where 1e-3 of a cell alone would approach the fp32
     error of the points; grid.hip's margin has an absolute floor), with and without the macro
-    grid (whole empty 8^3 blocks crossed in one skip; 'blob' = an object in empty space)."""
+    grid (whole empty 8^3 blocks crossed in one skip; 'blob' = an object in empty space).  The
+    one-pass form writes the points from the runs its counting walk recorded (16 per lane, then
+    the walk again: the dense grids' rays have far more runs) and must equal the two-pass form;
+    'tight' gives the round half the room it needs: every reserved position below cap holds its
+    ray's next occupied step, the overflowing rays keep their start step and gather again."""
     from nerf_amd._lib import lib, ptr, stream_of
     g = torch.Generator().manual_seed(31)
     N = 3000
@@ -539,10 +546,12 @@ def test_march_gather_empty_cell_skip_exact(cuda, ops, density, res, macro):
     f = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=cuda)  # noqa: E731
     T, rgb, dep, acc = f(N), f(N, 3), f(N), f(N)
     nxt, start, off, cnt = (f(N, dt=torch.int32) for _ in range(4))
+    if one_pass:
+        start = None
     alive, exh = f(N, dt=torch.uint8), f(N, dt=torch.uint8)
     counters = torch.zeros(2, dtype=torch.int32, device=cuda)
     evaluated = torch.zeros(1, dtype=torch.int64, device=cuda)
-    cap = int(occ.sum()) + 16
+    cap = int(occ.sum()) // 2 if tight else int(occ.sum()) + 16
     out_ray, out_step, out_pts = f(cap, dt=torch.int32), f(cap, dt=torch.int32), f(cap, 3)
     s = stream_of(rays)
     L = lib()
@@ -560,16 +569,27 @@ def test_march_gather_empty_cell_skip_exact(cuda, ops, density, res, macro):
                                ptr(acc), ptr(nxt), ptr(alive), ptr(exh), ptr(counters), ptr(evaluated), ptr(start),
                                ptr(out_ray), ptr(out_step), ptr(out_pts), ptr(off), ptr(cnt), cap, s) == 0
     n_pts = int(counters[0])
-    assert n_pts == int(occ.sum()) == int(evaluated[0])
-    c, o_ = cnt.cpu(), off.cpu()
-    steps, ray_ids = out_step[:n_pts].cpu(), out_ray[:n_pts].cpu()
+    assert n_pts == int(occ.sum())
+    n_written = min(n_pts, cap)
+    assert int(evaluated[0]) == n_written
+    c, o_, nx = cnt.cpu(), off.cpu(), nxt.cpu()
+    steps, ray_ids = out_step[:n_written].cpu(), out_ray[:n_written].cpu()
+    written = 0
     for r in range(N):
         want = torch.nonzero(occ[r]).flatten().int()
-        assert int(c[r]) == want.numel(), r
-        got = steps[int(o_[r]):int(o_[r]) + int(c[r])]
+        k = int(c[r])
+        if k < 0 or (tight and k == 0 and want.numel() > 0):  # overflowed: the part below cap, not composited
+            assert int(o_[r]) + want.numel() > cap and int(nx[r]) == 0, r
+            k = -k
+            want = want[:k]
+        else:
+            assert k == want.numel(), r
+        got = steps[int(o_[r]):int(o_[r]) + k]
         assert torch.equal(got, want), r
-        assert bool((ray_ids[int(o_[r]):int(o_[r]) + int(c[r])] == r).all())
-    np.testing.assert_array_equal(out_pts[:n_pts].cpu().numpy(),
+        assert bool((ray_ids[int(o_[r]):int(o_[r]) + k] == r).all())
+        written += k
+    assert written == n_written
+    np.testing.assert_array_equal(out_pts[:n_written].cpu().numpy(),
                                   pts.cpu()[ray_ids.long(), steps.long()].numpy())
 
 

@@ -59,11 +59,16 @@ def main():
                      for kl in (2, 4, 8) for tsp in (0.5, 0.9)]
         variants = [(n + (f"_sync{se}" if se != 4 else ""), sc, kl, tsp, se) for n, sc, kl, tsp in variants
                     for se in (4, 8)]
-        for name, sched, kl, tsp, se in variants:
+        # _2pass: gather + emit walking twice (round 2); _g<r>: k_low doubling from round r on
+        variants = [(n + sfx, sc, kl, tsp, se, op, gr) for n, sc, kl, tsp, se in variants
+                    for sfx, op, gr in (("", True, 0), ("_2pass", False, 0), ("_g4", True, 4), ("_g6", True, 6),
+                                        ("_g8", True, 8), ("_g10", True, 10))]
+        for name, sched, kl, tsp, se, op, gr in variants:
             if args.schedule and name not in args.schedule.split(","):
                 continue
             run = lambda: ops.march(net.model_fine.packer(), rays, 2.0, 6.0, grid, dtype=args.dtype,  # noqa: E731
-                                    k_schedule=sched, k_low=kl, t_split=tsp, sync_every=se)
+                                    k_schedule=sched, k_low=kl, t_split=tsp, sync_every=se, one_pass=op,
+                                    k_low_grow=gr)
             run()
             torch.cuda.synchronize()
             ts = []
