@@ -14,16 +14,16 @@ import json
 import sys
 
 LABELS = {
-    "fwd_kernel<nerf::mlp::PBF16, true, false>": "mlp_fwd_train",
-    "fwd_kernel<nerf::mlp::PF32, true, false>": "mlp_fwd_train",
-    "fwd_kernel<nerf::mlp::PBF16, false, false>": "mlp_fwd",
-    "fwd_kernel<nerf::mlp::PF32, false, false>": "mlp_fwd",
+    "fwd_kernel<nerf::mlp::PBF16, true, false,": "mlp_fwd_train",
+    "fwd_kernel<nerf::mlp::PF32, true, false,": "mlp_fwd_train",
+    "fwd_kernel<nerf::mlp::PBF16, false, false,": "mlp_fwd",
+    "fwd_kernel<nerf::mlp::PF32, false, false,": "mlp_fwd",
     "dx_kernel<nerf::mlp::PBF16>": "mlp_bwd_dx",
     "dx_kernel<nerf::mlp::PF32>": "mlp_bwd_dx",
     "dw_kernel<nerf::mlp::PBF16>": "mlp_bwd_dw",
     "dw_kernel<nerf::mlp::PF32>": "mlp_bwd_dw",
-    "fwd_kernel<nerf::mlp::PBF3, true, false>": "mlp_fwd_train",
-    "fwd_kernel<nerf::mlp::PBF3, false, false>": "mlp_fwd",
+    "fwd_kernel<nerf::mlp::PBF3, true, false,": "mlp_fwd_train",
+    "fwd_kernel<nerf::mlp::PBF3, false, false,": "mlp_fwd",
     "dx_kernel<nerf::mlp::PBF3>": "mlp_bwd_dx",
     "dw_kernel<nerf::mlp::PBF3>": "mlp_bwd_dw",
     "raygen_kernel(": "raygen",
