@@ -464,14 +464,6 @@ template <class P> __host__ __device__ constexpr int prefetch_depth() {
   return P::KIND == K_F32 ? NERF_PREFETCH_F32 : NERF_PREFETCH_BF16;  // a bf16 / bf16x3 step is 1-2 short MFMAs
 }
 constexpr int FINISH_DELAY = NERF_FINISH_DELAY;
-// Stagger of SIMD partners (MI355X_MICROARCH.md "Two waves that run the SAME program"): in the
-// 8-wave bf16 kernels waves w and w + 4 share a SIMD and would run their VALU finishes at the
-// same step; waves 4..7 issue theirs NERF_FINISH_DELAY_HI steps into the next unit instead (the
-// same instructions, placed where the partner is issuing MFMAs).  Outputs unchanged.
-#ifndef NERF_FINISH_DELAY_HI
-#define NERF_FINISH_DELAY_HI NERF_FINISH_DELAY
-#endif
-constexpr int FINISH_DELAY_HI = NERF_FINISH_DELAY_HI;
 
 // W: the wave object; it provides in_tile<u, t>(), prefetch<u>() (issue unit u's side
 // reads one unit ahead), init<u>(acc) (initial accumulator) and finish<u>(acc)
@@ -504,7 +496,7 @@ __host__ __device__ constexpr bool finished_in_group(int g, int u) {
 // W: the wave object; it provides in_tile<u, t>(), prefetch<u>() (issue unit u's side
 // reads one unit ahead), init<u>(acc) (initial accumulator), finish<u>(acc) and a
 // pending accumulator `pend` that carries a finished chain to its deferred finish
-template <class P, int DIR, bool DENSITY, int g, int FD = FINISH_DELAY, class W>
+template <class P, int DIR, bool DENSITY, int g, class W>
 __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
   constexpr int NS = group_steps<DIR, DENSITY, P::CH>(g);
   constexpr int PDP = prefetch_depth<P>();
@@ -535,7 +527,7 @@ __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
     acc = P::mma(a, w.template in_tile<S.u, S.t>(), S.c, acc);
     constexpr int U_BEFORE = S.j > 0 ? S.u - 1 : PREV_U;
     if constexpr (U_BEFORE >= 0 && finished_in_group<DIR, DENSITY, P::CH, cross_finish<P, DIR>()>(g, U_BEFORE) &&
-                  S.kin == (FD < S.len - 1 ? FD : S.len - 1))
+                  S.kin == (FINISH_DELAY < S.len - 1 ? FINISH_DELAY : S.len - 1))
       w.template finish<U_BEFORE>(w.pend);
     if constexpr (S.last && S.j == G.n - 1) {
       if constexpr (finished_in_group<DIR, DENSITY, P::CH, cross_finish<P, DIR>()>(g, S.u)) w.template finish<S.u>(acc);
@@ -917,18 +909,18 @@ struct FwdWave {
     finish_L<L, n>(acc);
   }
 
-  template <int g, int FD> __device__ __forceinline__ void step() {
+  template <int g> __device__ __forceinline__ void step() {
     constexpr int NG = GT::t.n;
     if constexpr (g + PF < NG) fetch<g + PF>();
     const uint32_t slot = lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024);
     wb = lds_ptr(slot + (uint32_t)(h * 16));
-    group_body<P, 0, DENSITY, g, FD>(*this, lds_ptr(slot + (uint32_t)(lane * 16)));
+    group_body<P, 0, DENSITY, g>(*this, lds_ptr(slot + (uint32_t)(lane * 16)));
     constexpr int N = handoff_vmcnt<P, 0, DENSITY>(g, [](int i) constexpr { return group_stores(i); },
                                                    STORE ? 3 * CH : 0);
     if constexpr (g + 1 < NG) wait_barrier<N>();
   }
 
-  template <int FD = FINISH_DELAY> __device__ __forceinline__ void run() {
+  __device__ __forceinline__ void run() {
     const int64_t ms = m < a.M ? m : a.M - 1;
     px = a.pts[ms * 3 + 0];
     py = a.pts[ms * 3 + 1];
@@ -961,7 +953,7 @@ struct FwdWave {
     settle(dx);
     settle(dy);
     settle(dz);
-    sfor<GT::t.n>([&](auto gg) { step<decltype(gg)::value, FD>(); });
+    sfor<GT::t.n>([&](auto gg) { step<decltype(gg)::value>(); });
     if (h == 0 && m < a.M)
       *(float4*)(a.raw + m * 4) = DENSITY ? make_float4(0.f, 0.f, 0.f, alpha) : make_float4(rgb0, rgb1, rgb2, alpha);
   }
@@ -980,24 +972,13 @@ __device__ __forceinline__ void young_priority() {
 // march's gather count: no host round trip sizes the launch) and a grid of one wave of
 // workgroups loops over the sample blocks; the barrier at the end of each block keeps the next
 // block's prologue DMA out of the ring slot still being read.
-// run the wave's body with its finish delay: waves 4..7 of an 8-wave workgroup (the SIMD
-// partners of waves 0..3) use FINISH_DELAY_HI
-template <class P, class W> __device__ __forceinline__ void run_staggered(W& w) {
-  if constexpr (P::WAVES == 8 && FINISH_DELAY_HI != FINISH_DELAY) {
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) w.template run<FINISH_DELAY_HI>();
-    else w.template run<FINISH_DELAY>();
-  } else {
-    w.template run<FINISH_DELAY>();
-  }
-}
-
 template <class P, bool STORE, bool DENSITY, bool PERSIST>
 __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
   young_priority();
   if constexpr (!PERSIST) {
     FwdWave<P, STORE, DENSITY> w(a, smem_u4, blockIdx.x, threadIdx.x);
-    run_staggered<P>(w);
+    w.run();
   } else {
     static_assert(!STORE, "the persistent forward is inference only");
     const int64_t cnt = a.M_dev[0];
@@ -1010,7 +991,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
       int tid = threadIdx.x;
       asm volatile("" : "+v"(tid));
       FwdWave<P, STORE, DENSITY, true> w(b, smem_u4, blk, tid);
-      run_staggered<P>(w);
+      w.run();
       __syncthreads();
     }
   }
@@ -1128,16 +1109,16 @@ struct DxWave {
     store_tile<P>(a.dz, a.nblk, ZT_TILES, dzt, wblock, lane, out);
   }
 
-  template <int g, int FD> __device__ __forceinline__ void step() {
+  template <int g> __device__ __forceinline__ void step() {
     constexpr int NG = GT::t.n;
     if constexpr (g + PF < NG) fetch<g + PF>();
     const uint32_t slot = lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024);
-    group_body<P, 1, false, g, FD>(*this, lds_ptr(slot + (uint32_t)(lane * 16)));
+    group_body<P, 1, false, g>(*this, lds_ptr(slot + (uint32_t)(lane * 16)));
     constexpr int N = handoff_vmcnt<P, 1, false>(g, [](int i) constexpr { return group_stores(i); }, 2 * CH);
     if constexpr (g + 1 < NG) wait_barrier<N>();
   }
 
-  template <int FD = FINISH_DELAY> __device__ __forceinline__ void run() {
+  __device__ __forceinline__ void run() {
     // output gradients of rgb_linear (rows 0..2) and alpha_linear (row 0): lanes 0..31
     const float4 gr = m < a.M ? *(const float4*)(a.d_raw + m * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -1165,7 +1146,7 @@ struct DxWave {
       settle(mk[i].z);
       settle(mk[i].w);
     }
-    sfor<GT::t.n>([&](auto gg) { step<decltype(gg)::value, FD>(); });
+    sfor<GT::t.n>([&](auto gg) { step<decltype(gg)::value>(); });
   }
 };
 
@@ -1174,7 +1155,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
   young_priority();
   DxWave<P> w(a, smem_u4);
-  run_staggered<P>(w);
+  w.run();
 }
 
 // ------------------------------------------------------------------------------------

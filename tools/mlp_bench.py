@@ -157,6 +157,17 @@ def compare(args):
                 if r:
                     times[(name, k)].append(a.elapsed_time(e) / args.reps)
     out = {"M": M, "rounds": args.rounds}
+    # the builds must compute the same thing: forward raw, the stored activations and the dX
+    # stores, bit for bit (buffers zeroed first: padding a kernel never writes stays equal)
+    n0 = libs[0][0]
+    for name, L in libs:
+        for key in ("raw", "act", "masks", "dz"):
+            bufs[name][key].zero_()
+        kernels(L, bufs[name])["fwd_train"]()
+        kernels(L, bufs[name])["dx"]()
+    torch.cuda.synchronize()
+    out["identical_to_" + n0] = {name: {key: bool(torch.equal(bufs[name][key], bufs[n0][key]))
+                                        for key in ("raw", "act", "masks", "dz")} for name, _ in libs[1:]}
     for name, _ in libs:
         out[name] = {k: round(statistics.median(times[(name, k)]), 4) for k in ("fwd", "fwd_train", "dx", "dw")}
     print(json.dumps(out), flush=True)
