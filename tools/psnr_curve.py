@@ -6,6 +6,12 @@ Adam) and the reference's ExponentialLR (lr 5e-4 x 0.1^(epoch/500), stepped ever
 train.py:43-46).  Prints a progress line per evaluation and writes gpurun_out/psnr_curve.json.
 
     python tools/psnr_curve.py [--steps 15000] [--every 1000] [--dtypes fp32,bf16x3,bf16]
+
+A run longer than one GPU call (config 3's 200k steps: 94 min at fp32) continues across calls:
+--ckpt-out DIR saves <dtype>.pt (weights, the reference-format Adam state, scheduler, the ray
+stream's and the renderer's Philox counters, the curve so far) at every evaluation and when
+--max-seconds of wall time are used up; --ckpt-in DIR resumes from it (same ray stream, same
+schedule).
 """
 import argparse
 import json
@@ -27,7 +33,11 @@ def main():
     ap.add_argument("--every", type=int, default=1000)
     ap.add_argument("--epoch_steps", type=int, default=500)
     ap.add_argument("--dtypes", default="fp32,bf16x3,bf16")
+    ap.add_argument("--ckpt-in", default=None)
+    ap.add_argument("--ckpt-out", default=None)
+    ap.add_argument("--max-seconds", type=float, default=0.0)
     args = ap.parse_args()
+    t_start = time.time()
     dev = torch.device("cuda:0")
     from nerf_amd import ops
     from src.config import cfg
@@ -73,8 +83,35 @@ def main():
         opt = make_optimizer(cfg, net)
         sched = ExponentialLR(opt, decay_epochs=500, gamma=0.1)
         ds = Dataset.from_arrays(imgs, poses, focal)
-        curve, t_train = [], 0.0
-        for step in range(1, args.steps + 1):
+        curve, t_train, first = [], 0.0, 1
+        renderer = trainer.network.renderer
+        src = os.path.join(args.ckpt_in, f"{dtype}.pt") if args.ckpt_in else None
+        if src and os.path.exists(src):
+            ck = torch.load(src, map_location="cpu", weights_only=True)
+            net.load_state_dict(ck["net"], strict=True)
+            opt.load_state_dict(ck["optim"])
+            sched.load_state_dict(ck["sched"])
+            ds.draws, renderer._calls = int(ck["draws"]), int(ck["calls"])
+            curve, t_train, first = [tuple(x) for x in ck["curve"].tolist()], float(ck["t_train"]), int(ck["step"]) + 1
+            ops.params_updated()
+            print(json.dumps({"dtype": dtype, "resumed_at": first - 1}), flush=True)
+
+        def save(step):
+            if not args.ckpt_out:
+                return
+            os.makedirs(args.ckpt_out, exist_ok=True)
+            tmp = os.path.join(args.ckpt_out, f"{dtype}.pt.tmp")
+            torch.save({"net": {k: v.detach().cpu() for k, v in net.state_dict().items()}, "optim": opt.state_dict(),
+                        "sched": sched.state_dict(), "draws": ds.draws, "calls": renderer._calls, "step": step,
+                        "curve": torch.tensor(curve, dtype=torch.float64).reshape(-1, 2), "t_train": t_train}, tmp)
+            os.replace(tmp, os.path.join(args.ckpt_out, f"{dtype}.pt"))
+        stopped = False
+        for step in range(first, args.steps + 1):
+            if args.max_seconds and time.time() - t_start > args.max_seconds:
+                save(step - 1)
+                print(json.dumps({"dtype": dtype, "paused_at": step - 1}), flush=True)
+                stopped = True
+                break
             rays, rgbs = ds.sample_batch()
             t0 = time.perf_counter()
             trainer.train_step({"rays": rays[None], "rgbs": rgbs[None], "near": ops.device_scalar(2.0, dev),
@@ -87,13 +124,16 @@ def main():
                 p = heldout(net)
                 curve.append((step, round(p, 3)))
                 print(json.dumps({"dtype": dtype, "step": step, "psnr": round(p, 3)}), flush=True)
+                save(step)
             else:
                 t_train += time.perf_counter() - t0
-        out[f"psnr_curve_{dtype}"] = curve
+        if stopped:
+            break
+        out[f"psnr_curve_{dtype}"] = [[int(a), float(b)] for a, b in curve]
         out[f"train_s_{dtype}"] = round(t_train, 1)
         del net, trainer, opt, ds
         torch.cuda.empty_cache()
-    dts = args.dtypes.split(",")
+    dts = [d for d in args.dtypes.split(",") if f"psnr_curve_{d}" in out]
     if "fp32" in dts:
         for dt in dts:
             if dt == "fp32":
@@ -105,7 +145,8 @@ def main():
             out[f"mean_delta_db_last_third_{dt}"] = round(float(np.mean([y[1] - x[1] for x, y in
                                                                          zip(a[-tail:], b[-tail:])])), 3)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "psnr_curve.json"), "w") as f:
+    with open(os.path.join(args.ckpt_out or os.path.join(ROOT, "gpurun_out"),
+                           "psnr_curve_" + "_".join(dts) + ".json" if args.ckpt_out else "psnr_curve.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out), flush=True)
 
