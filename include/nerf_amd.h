@@ -174,7 +174,7 @@ int64_t nerf_march_macro_bytes(int res);
 int nerf_march_macro(const uint8_t* grid, int res, uint8_t* macro, hipStream_t stream);
 /* start_step_scratch: null = one pass (the counting walk records its points as runs of occupied
  * steps and writes them after the reservation; the default), or an [N] int32 workspace = the
- * two-pass form (a second walk writes the points).  Same outputs.  n_steps < 65536. */
+ * two-pass form (a second walk writes the points).  Same outputs.  One pass needs n_steps < 65536. */
 int nerf_march_gather(const float* rays, int64_t N, const float* t_table, int n_steps, const uint8_t* grid, int res,
                       const uint8_t* macro, const float* bbox_host, int K, int k_low, float t_split, float* T,
                       float* rgb, float* depth,

@@ -665,8 +665,8 @@ int nerf_march_gather(const float* rays, int64_t N, const float* t_table, int n_
   MarchGatherArgs a{rays, N, t_table, n_steps, grid, res, macro, make_bbox(bbox_host), K, k_low, t_split,
                     {T, rgb, depth, acc, next_step, alive, exhausted},
                     counters, evaluated, out_ray, out_step, out_pts, ray_off, ray_cnt, cap};
-  NERF_REQUIRE(n_steps < 65536, "nerf_march_gather: n_steps must be < 65536 (16-bit run starts)");
   if (!start_step_scratch) {  // one pass: gather + emit fused (march_gather_emit_kernel)
+    NERF_REQUIRE(n_steps < 65536, "nerf_march_gather: the one-pass form needs n_steps < 65536 (16-bit run starts)");
     hipLaunchKernelGGL(march_gather_emit_kernel, grid1(N), dim3(256), 0, stream, a);
     return check_launch("nerf_march_gather");
   }

@@ -620,6 +620,7 @@ def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: 
     nxt = torch.empty(N, dtype=torch.int32, device=dev)
     alive = torch.empty(N, dtype=torch.uint8, device=dev)
     exh = torch.empty(N, dtype=torch.uint8, device=dev)
+    one_pass = one_pass and n_steps < 65536  # (the one-pass runs hold 16-bit step indices)
     start = None if one_pass else torch.empty(N, dtype=torch.int32, device=dev)
     off = torch.empty(N, dtype=torch.int32, device=dev)
     cnt = torch.empty(N, dtype=torch.int32, device=dev)
