@@ -168,6 +168,13 @@ def compare(args):
     torch.cuda.synchronize()
     out["identical_to_" + n0] = {name: {key: bool(torch.equal(bufs[name][key], bufs[n0][key]))
                                         for key in ("raw", "act", "masks", "dz")} for name, _ in libs[1:]}
+    # and the inference forward's output
+    for name, L in libs:
+        bufs[name]["raw"].zero_()
+        kernels(L, bufs[name])["fwd"]()
+    torch.cuda.synchronize()
+    for name, _ in libs[1:]:
+        out["identical_to_" + n0][name]["raw_inference"] = bool(torch.equal(bufs[name]["raw"], bufs[n0]["raw"]))
     for name, _ in libs:
         out[name] = {k: round(statistics.median(times[(name, k)]), 4) for k in ("fwd", "fwd_train", "dx", "dw")}
     print(json.dumps(out), flush=True)
