@@ -21,5 +21,5 @@ PY
 fi
 CKIN=""
 if [ -f ckpt/psnr200k/$DT.pt ]; then CKIN="--ckpt-in ckpt/psnr200k"; fi
-timeout -k 10 1080 python3 -u tools/psnr_curve.py --dtypes $DT --steps 200000 --every 5000 $CKIN --ckpt-out gpurun_out/psnr200k --max-seconds ${PSNR_SECONDS:-960} > gpurun_out/psnr200k/run_$DT.log 2>&1
+timeout -k 10 1150 python3 -u tools/psnr_curve.py --dtypes $DT --steps 200000 --every 5000 $CKIN --ckpt-out gpurun_out/psnr200k --max-seconds ${PSNR_SECONDS:-960} > gpurun_out/psnr200k/run_$DT.log 2>&1
 r=$?; tail -4 gpurun_out/psnr200k/run_$DT.log; exit $r
