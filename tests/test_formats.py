@@ -236,3 +236,38 @@ def test_blender_loader_rays_on_gpu(tmp_path, cuda):
         np.testing.assert_array_equal(rays[:, :3].cpu().numpy(), o.reshape(-1, 3).numpy())
         np.testing.assert_allclose(rays[:, 3:].cpu().numpy(), d.reshape(-1, 3).numpy(), rtol=0, atol=2e-7)
         np.testing.assert_array_equal(rgbs.cpu().numpy(), imgs[k].reshape(-1, 3))
+
+
+def test_evaluator_host_path_pngs_and_summary(tmp_path):
+    """The Evaluator fed host arrays (evaluators/nerf.py:47-92 of the reference): PSNR =
+    -10 log10(mse) on the float images, the PNG pair holds what the reference's cv2.imwrite calls
+    store -- saturate_cast (round half to even, clamp) of pred x 255, and its uint8 gt x 255
+    wrapped modulo 256 -- and summarize() writes summary.json {mean_psnr, mean_ssim}."""
+    from PIL import Image
+    from src.config import cfg
+    from src.evaluators import nerf as ev_mod
+    old = cfg.result_dir
+    cfg.result_dir = str(tmp_path)
+    try:
+        H, W = 24, 20
+        g = torch.Generator().manual_seed(9)
+        gt = torch.rand(1, H * W, 3, generator=g)
+        pred = gt[0] + 0.05 * torch.randn(H * W, 3, generator=g)  # unclamped, as rendered (white bkgd can pass 1)
+        pred[0] = torch.tensor([0.5 / 255, 1.5 / 255, 1.002])  # halves round to even; > 1 saturates
+        e = ev_mod.Evaluator()
+        out = e.evaluate({"rgb_map_f": pred}, {"rgbs": gt, "i": torch.tensor([7]), "H": torch.tensor([H]),
+                                                "W": torch.tensor([W])})
+        p, t = pred.reshape(H, W, 3).numpy(), gt.reshape(H, W, 3).numpy()
+        assert out["psnr"] == pytest.approx(-10 * np.log(np.mean((p - t) ** 2)) / np.log(10), rel=1e-12)
+        png = np.asarray(Image.open(tmp_path / "images" / "view007_pred.png"))
+        np.testing.assert_array_equal(png, np.clip(np.rint(p * np.float32(255)), 0, 255).astype(np.uint8))
+        assert tuple(png[0, 0]) == (0, 2, 255)
+        g8 = (t * 255).astype(np.uint8)
+        np.testing.assert_array_equal(np.asarray(Image.open(tmp_path / "images" / "view007_gt.png")),
+                                      ((g8.astype(np.int64) * 255) % 256).astype(np.uint8))
+        s = e.summarize()
+        with open(tmp_path / "summary.json") as f:
+            saved = json.load(f)
+        assert saved == {"mean_psnr": pytest.approx(s["psnr"]), "mean_ssim": pytest.approx(s["ssim"])}
+    finally:
+        cfg.result_dir = old
