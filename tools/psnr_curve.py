@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--ckpt-in", default=None)
     ap.add_argument("--ckpt-out", default=None)
     ap.add_argument("--max-seconds", type=float, default=0.0)
+    ap.add_argument("--seed", type=int, default=0, help="torch seed: initial weights and the ray / sample streams")
     args = ap.parse_args()
     t_start = time.time()
     dev = torch.device("cuda:0")
@@ -71,13 +72,13 @@ def main():
         cfg.task_arg.perturb = 1
         return float(np.mean(ps))
 
-    out = {"steps": args.steps, "every": args.every, "rays_per_step": int(cfg.task_arg.train_rays),
+    out = {"seed": args.seed, "steps": args.steps, "every": args.every, "rays_per_step": int(cfg.task_arg.train_rays),
            "epoch_steps": args.epoch_steps, "lr": "5e-4 x 0.1^(epoch/500)", "heldout_views": 4, "res": 100,
            "scene": "procedural (src/datasets/nerf/synthetic.py make_scene seed 0), 100 views 100x100"}
     for dtype in args.dtypes.split(","):
         cfg.task_arg.mlp_dtype = dtype
         cfg.task_arg.perturb = 1
-        torch.manual_seed(0)
+        torch.manual_seed(args.seed)
         net = make_network(cfg)
         trainer = make_trainer(cfg, net)
         opt = make_optimizer(cfg, net)
