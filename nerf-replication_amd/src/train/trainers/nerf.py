@@ -5,7 +5,6 @@ with loss = MSE(rgb_map_c, gt) + MSE(rgb_map_f, gt).  Like the reference it buil
 Renderer from this module path directly (nerf.py:3,10), so the drop-in renderer must live
 at src.models.nerf.renderer.volume_renderer.
 """
-import torch
 import torch.nn as nn
 
 from src.models.nerf.renderer.volume_renderer import Renderer

@@ -8,7 +8,6 @@ import os
 import sys
 
 import torch
-import yaml
 
 
 def _pths(model_dir):

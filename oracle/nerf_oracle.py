@@ -27,7 +27,6 @@ fixtures in ``tests/golden/*.npz``; test ``tests/test_oracle_golden.py``).
 """
 from __future__ import annotations
 
-import math
 from dataclasses import dataclass
 from typing import Dict, Optional
 
