@@ -56,7 +56,7 @@ def main():
         ref = None
         variants = [(n, sc, 1024, 2.0) for n, sc in SCHEDULES.items()]  # t_split 2: k_low never used
         variants += [(f"{n}_klow{kl}_t{tsp}", SCHEDULES[n], kl, tsp) for n in ("12x2", "16x2")
-                     for kl in (2, 4, 8) for tsp in (0.5, 0.9)]
+                     for kl in (2, 4, 8, 16) for tsp in (0.5, 0.7, 0.9)]
         variants = [(n + (f"_sync{se}" if se != 4 else ""), sc, kl, tsp, se) for n, sc, kl, tsp in variants
                     for se in (4, 8)]
         # _2pass: gather + emit walking twice (round 2); _g<r>: k_low doubling from round r on
