@@ -43,9 +43,14 @@ KEYS = ["rgb_map_c", "depth_map_c", "acc_map_c", "rgb_map_f", "depth_map_f", "ac
 # *same* CDF (north_star: indices bit-exact for identical CDF inputs) the fine pass is held to
 # 1e-4 below (test_fine_pass_given_reference_samples).
 E2E_FINE_DEPTH_TOL = 6e-4
+# Everything else is held to the measured error with ~5-10x margin (MI355X, round 3: fp32
+# coarse/rgb/acc <= 1.5e-6, fine depth 2.5e-4; bf16 rgb/acc <= 1.4e-4, coarse depth 2.3e-4,
+# fine depth 6.1e-3 -- bf16 moves more fine samples to the neighbouring bin).
+E2E_TOL = 1e-5
+BF16_TOL = {"depth_map_c": 1.5e-3, "depth_map_f": 1.2e-2}
 
 
-@pytest.mark.parametrize("dtype,tol", [("fp32", 1e-4), ("bf16", 2e-3)])
+@pytest.mark.parametrize("dtype,tol", [("fp32", E2E_TOL), ("bf16", 5e-4)])
 def test_render_perturb0(golden, cuda, stack, dtype, tol):
     cfg, net, r = stack
     cfg.task_arg.mlp_dtype = dtype
@@ -54,7 +59,7 @@ def test_render_perturb0(golden, cuda, stack, dtype, tol):
         out = r.render(_batch(golden, cuda))
     for k in KEYS:
         ref = golden[f"render0_{k}"]
-        t = tol * (6.0 if "depth" in k else 1.0) if dtype == "bf16" else tol
+        t = BF16_TOL.get(k, tol) if dtype == "bf16" else tol
         if k == "depth_map_f" and dtype == "fp32":
             t = E2E_FINE_DEPTH_TOL
         np.testing.assert_allclose(out[k].cpu().numpy(), ref, rtol=0, atol=t, err_msg=k)
@@ -97,7 +102,7 @@ def test_render_perturb1_injected(golden, cuda, stack, O=None):
     got = dict(rgb_map_c=rgb_c, depth_map_c=dep_c, acc_map_c=acc_c, rgb_map_f=rgb_f, depth_map_f=dep_f,
                acc_map_f=acc_f)
     for k in KEYS:
-        t = E2E_FINE_DEPTH_TOL if k == "depth_map_f" else 1e-4
+        t = E2E_FINE_DEPTH_TOL if k == "depth_map_f" else E2E_TOL
         np.testing.assert_allclose(got[k].cpu().numpy(), golden[f"render1_{k}"], rtol=0, atol=t, err_msg=k)
 
 
@@ -115,10 +120,13 @@ def test_loss_gradients_match_reference(golden, cuda, stack):
     for i, name in enumerate(golden["grad_names"]):
         g = params[str(name)].grad.reshape(-1).cpu()
         norm = float(torch.linalg.vector_norm(g.double()))
-        np.testing.assert_allclose(norm, golden["grad_norms"][i], rtol=2e-3, err_msg=str(name))
         sel = g[torch.from_numpy(golden["grad_sel_idx"][i])].numpy()
         scale = np.abs(golden["grad_sel_val"][i]).max() + 1e-12
-        assert np.abs(sel - golden["grad_sel_val"][i]).max() / scale < 5e-3, name
+        # coarse grads see no resampling: measured <= 1.1e-6 (norm) / 4.2e-6 (entries);
+        # fine grads inherit the fine-sample moves above: <= 2.9e-4 / 7.3e-4
+        rn, rs = (2e-3, 4e-3) if str(name).startswith("model_fine.") else (1e-5, 4e-5)
+        np.testing.assert_allclose(norm, golden["grad_norms"][i], rtol=rn, err_msg=str(name))
+        assert np.abs(sel - golden["grad_sel_val"][i]).max() / scale < rs, name
     net.zero_grad()
 
 
@@ -140,10 +148,12 @@ def test_render_accelerated_real_grid(golden, cuda, stack, tag):
         net.model_fine.alpha_linear.bias += bias
         out = r.render_accelerated({"rays": rays[None], "near": torch.tensor([2.0]), "far": torch.tensor([6.0])})
         net.model_fine.alpha_linear.bias -= bias
-    assert out["n_queried"] >= int(golden[f"march_{tag}_queried"])
+    # n_queried counts composited points (the reference's pts_mask count): equal, and the maps
+    # within 5x of the measured error (rgb/acc <= 2.3e-6, depth <= 1.0e-5)
+    assert out["n_queried"] == int(golden[f"march_{tag}_queried"])
     for k in ("rgb_map_f", "depth_map_f", "acc_map_f"):
         np.testing.assert_allclose(out[k].cpu().numpy(), golden[f"march_{tag}_{k}"], rtol=0,
-                                   atol=1e-4 * (6 if "depth" in k else 1), err_msg=k)
+                                   atol=5e-5 if "depth" in k else 1e-5, err_msg=k)
 
 
 def test_grid_occupancy_lookup(golden, cuda):
