@@ -197,3 +197,24 @@ def test_render_video_frames(cuda, stack):
     for f in frames:
         assert f.shape == (48, 48, 3) and f.dtype == np.uint8
     assert not np.array_equal(frames[0], frames[1])  # the camera moved
+
+
+def test_march_repeat_frames_and_grid_change(golden, cuda, stack):
+    """Two frames of the same rays and grid are bit-identical (counts included), and an
+    in-place change of the grid is seen by the next frame.  (Keeping the uint8 grid, its macro
+    blocks and the work buffers between frames was measured and not kept: bf16 0.0148 s vs
+    0.0146 s per 800x800 frame -- the launches run ahead of the GPU, host setup is hidden.)"""
+    from nerf_amd import ops
+    cfg, net, r = stack
+    grid = _real_grid().to(cuda)
+    rays = torch.from_numpy(golden["march_rays"]).to(cuda)
+    p = net.model_fine.packer()
+    with torch.no_grad():
+        a = ops.march(p, rays, 2.0, 6.0, grid)
+        b = ops.march(p, rays, 2.0, 6.0, grid)
+        grid.zero_()
+        c = ops.march(p, rays, 2.0, 6.0, grid)
+    for k in ("rgb_map_f", "depth_map_f", "acc_map_f"):
+        assert torch.equal(a[k], b[k]), k
+    assert a["n_queried"] == b["n_queried"] > 0 and a["n_evaluated"] == b["n_evaluated"]
+    assert c["n_queried"] == 0 and float(c["acc_map_f"].abs().max()) == 0.0
