@@ -55,9 +55,11 @@ PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3}
 STREAM_KERNELS = ("raygen", "sample_stratified", "sample_pdf", "composite_fwd", "composite_bwd")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a torch.distributed environment, N > 1 starts "
+                         "torch.distributed.run as a child process (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU per step")
@@ -71,7 +73,48 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=1024)
     ap.add_argument("--detail-steps", type=int, default=5,
                     help="extra untimed steps that time the sampling/compositing kernels (after the timed region)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(gpus: int, argv, port: int):
+    """The torch.distributed.run command that runs this script as ``gpus`` ranks on one node
+    (the driver's own form: --nnodes=1, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(gpus, env=os.environ):
+    """(world size this process runs at, error or None).  Under torch.distributed.run the world
+    is WORLD_SIZE; an explicit --gpus that disagrees with it is an error (the bench would
+    otherwise report a rank count nobody asked for)."""
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if gpus is not None and gpus != world:
+            return world, f"--gpus {gpus} but WORLD_SIZE={world}: launch with --nproc-per-node {gpus}"
+        return world, None
+    return (1 if gpus is None else gpus), None
+
+
+def launch_ranks(gpus: int, argv) -> int:
+    """--gpus N > 1 in a plain process: start torch.distributed.run with N ranks as a CHILD
+    process (never an exec; this process has made no GPU call), relay rank 0's stdout (the
+    JSON line) and return the child's exit status."""
+    cmd = launcher_command(gpus, argv, free_port())
+    log("launching " + " ".join(cmd))
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    for line in proc.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return proc.wait()
 
 
 def pmc_traffic(kernel, dtype):
@@ -102,7 +145,36 @@ def setup_dist():
             dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend, init_method="env://")
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
     return world, rank, torch.device("cuda", local)
+
+
+def gather_floats(x: float, device):
+    """[x of rank 0, x of rank 1, ...] (rank order)."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return [x]
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [float(p) for p in parts]
+
+
+def allreduce_standalone(n: int, device, reps: int = 20):
+    """Mean ms of one SUM all-reduce of an n-float fp32 buffer (the flat gradient's size) on
+    this process group, outside the training step: the link cost the step hides."""
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    g = torch.ones(n, dtype=torch.float32, device=dev)
+    for _ in range(3):
+        dist.all_reduce(g)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_reduce(g)
+    if dev != "cpu":
+        torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
 
 
 def build(args, device, dtype):
@@ -207,6 +279,7 @@ def measure_training(args, world, rank, device, dtype):
         train_step(cfg, trainer, opt, ds, device)
     if world > 1:
         dist.barrier()
+        trainer.buckets.events = []
     torch.cuda.synchronize()
     ops.KERNEL_TIMES.reset()
     ops.KERNEL_TIMES.enabled = True
@@ -218,10 +291,20 @@ def measure_training(args, world, rank, device, dtype):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     ops.KERNEL_TIMES.enabled = False
+    dist_info = None
     if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+        per_rank = gather_floats(elapsed / args.steps * 1e3, device)
+        exposed = gather_floats(trainer.buckets.exposed_ms() or 0.0, device)
+        trainer.buckets.events = None
+        elapsed = max(per_rank) * args.steps / 1e3
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                     "ms_per_step_per_rank": [round(x, 3) for x in per_rank],
+                     "allreduce_exposed_ms_per_step_per_rank": [round(x, 4) for x in exposed],
+                     "allreduce_standalone_ms": round(allreduce_standalone(opt.flat_grad.numel(), device), 4),
+                     "allreduce_bytes": opt.flat_grad.numel() * 4,
+                     "note": "exposed = compute-stream time in GradBuckets.finish (wait for the per-net "
+                             "buckets + 1/W scale), HIP events; standalone = one all-reduce of the flat "
+                             "gradient's size outside the step"}
     ktimes = {k: v for k, v in ops.KERNEL_TIMES.summary().items() if k not in STREAM_KERNELS}
     train_stream = detail_times(lambda: [train_step(cfg, trainer, opt, ds, device) for _ in range(args.detail_steps)],
                                 dtype) if args.detail_steps > 0 else {}
@@ -238,7 +321,7 @@ def measure_training(args, world, rank, device, dtype):
                     traffic_vs_mlp_io=None if traffic is None else round(traffic / io_bytes, 1))
     kt = {k: {"launches": n, "avg_ms": round(m / n, 4), "roofline": mlp_roofline(k, n, m, u, dtype),
               "hbm": hbm_roofline(k, n, m, dtype)} for k, (n, m, u) in ktimes.items()}
-    return value, elapsed / args.steps * 1e3, roofline, kt, train_stream, (cfg, net, ds)
+    return value, elapsed / args.steps * 1e3, roofline, kt, train_stream, (cfg, net, ds), dist_info
 
 
 def render_frame_time(cfg, net, ds, device, world, reps=2):
@@ -526,12 +609,19 @@ def eager_gpu_baseline(device, n_rays, dtype, reps=11):
 
 def main():
     args = parse()
+    want, err = check_world(args.gpus)
+    if err is not None:
+        log(err)
+        sys.exit(2)
+    if want > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(want, sys.argv[1:]))
     world, rank, device = setup_dist()
     others = [] if args.no_second else [d for d in ("fp32", "bf16x3", "bf16") if d != args.dtype]
     lines = {}
     for dtype in [args.dtype] + others:
         log(f"training {dtype}: {args.warmup} warmup + {args.steps} timed steps")
-        value, ms_step, roofline, kt, train_stream, (cfg, net, ds) = measure_training(args, world, rank, device, dtype)
+        value, ms_step, roofline, kt, train_stream, (cfg, net, ds), dist_info = \
+            measure_training(args, world, rank, device, dtype)
         render_s, render_stream, grid = None, None, None
         log(f"{dtype}: {value:.0f} rays/s")
         if not args.no_render:
@@ -551,6 +641,7 @@ def main():
             "stream_kernels": {"train_step": train_stream, "render_800x800": render_stream},
             "render_s_per_frame": None if render_s is None else round(render_s, 4),
             "render_parallelism": f"tile-split over {world} GPU(s)", "occupancy_grid": grid,
+            "distributed": dist_info,
         }
         del net, ds
         torch.cuda.empty_cache()

@@ -100,7 +100,11 @@ __device__ __forceinline__ float wave_sum(float v) {
 // n/8: row_sum's ilp-4 partials p_k = sum_r v_{4r+k} (r < nv/4, multi_row_sum below its first
 // 16-row level), the leftover vectors added to p_0, then p_0 + p_1 + p_2 + p_3; the scalar tail
 // x[8nv, n) summed from 0, then the 8 vector lanes added in order.  Matches torch 2.10 CPU on
-// every one of 20,000 random 62-value rows (tree sum: 52 %, fp64: 57 %).
+// every one of 20,000 random 62-value rows (tree sum: 52 %, fp64: 57 %).  The order is that of
+// torch CPU with 8-float vectors: on the x86 host the goldens were made on (AVX512-capable),
+// ATEN_CPU_CAPABILITY=avx512 / avx2 / default give the same sums bit for bit (sum_stub runs
+// on 32-byte vectors in all three); a build with 16-float sum vectors, or the reference run
+// on CUDA (another reduction order), is not what this pins.
 __device__ __forceinline__ float torch_row_sum(float x, int n) {
   const int j = lane_id() & 7;
   const int nv = n >> 3, nilp = nv >> 2;

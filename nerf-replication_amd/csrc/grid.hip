@@ -174,7 +174,8 @@ __device__ __forceinline__ bool march_occupied(const MarchGatherArgs& a, const f
 // boundary cells that also hold the clamped outside -- and the computed p = o + t d is monotone
 // in t.  Every step whose t is below the first exit of the interval SHRUNK by a margin m is
 // therefore in the same empty cell, and is skipped; the walk resumes one step at a time near the
-// boundary.  m = max(1e-3 w, 2^-18 (|o| + 8 |d| + |mn| + |mx|)): 1e-3 w is ~2.4e-5 at res 128, but
+// boundary.  m = max(1e-3 w, 2^-18 (|o| + t_abs |d| + |mn| + |mx|)), t_abs = max(8, |t| over the
+// table) (a far bound past 8 widens the margin with the coordinates): 1e-3 w is ~2.4e-5 at res 128, but
 // shrinks as 1/res (2.9e-6 at res 1024), while the fp32 errors of p = o + t d, of the interval
 // bounds and of t_exit d are a few ulps of the coordinates' magnitude (~1e-6 for |o| ~ 4, t <= 6
 // here): the absolute floor keeps the margin >= 8 such ulps at any resolution.  Returns the next
@@ -187,13 +188,15 @@ __device__ __forceinline__ bool march_occupied(const MarchGatherArgs& a, const f
 constexpr int MACRO = 8;
 __device__ __forceinline__ int march_skip_empty(const MarchGatherArgs& a, const float* ray, int s, const int* cell,
                                                 int span) {
-  // fp32 with approximate reciprocals: the errors (~1e-6 in p) are far inside the margin
+  // fp32 with approximate reciprocals: the errors (~1e-6 in p) are far inside the margin.
+  // |t| is bounded by the table's ends (it is monotone); 8 is the floor the bound was tested at
+  const float t_abs = fmaxf(8.0f, fmaxf(fabsf(a.t_table[0]), fabsf(a.t_table[a.n_steps - 1])));
   float t_exit = 3.0e38f;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const float d = ray[3 + k];
     const float mn = a.bb.mn[k], w = (a.bb.mx[k] - mn) * (1.0f / (float)(a.res - 1));
-    const float mag = fabsf(ray[k]) + 8.0f * fabsf(d) + fabsf(mn) + fabsf(a.bb.mx[k]);
+    const float mag = fabsf(ray[k]) + t_abs * fabsf(d) + fabsf(mn) + fabsf(a.bb.mx[k]);
     const float m = fmaxf(1e-3f * w, mag * 3.814697265625e-6f);  // 2^-18
     const int lo = cell[k] / span * span, hi = min(lo + span - 1, a.res - 1);  // the interval's cells
     const float rd = __builtin_amdgcn_rcpf(d);

@@ -598,7 +598,12 @@ def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: 
     0.0172 s two-pass / 0.0155 one-pass / 0.0146 with k_low_grow 8, tools/march_bench.py,
     profiles/r3/march_sweep.json).  n_queried
     counts the composited points only -- exactly the reference's MLP queries
-    (volume_renderer.py:324) -- and n_evaluated every point the MLP ran on."""
+    (volume_renderer.py:324) -- and n_evaluated every point the MLP ran on.  ``rounds`` counts
+    the rounds that had live rays (``rounds_launched`` also counts the up to sync_every - 1
+    empty rounds after the last one).  The point buffer is sized once per call for the
+    largest round the byte budget allows (up to round_bytes, ~2.1 GB at the default); it
+    comes from PyTorch's caching allocator, so consecutive frames (and in-training
+    validation) reuse one block rather than allocating it again."""
     rays = _f32c(rays.reshape(-1, 6), "rays")
     dev, N = rays.device, rays.shape[0]
     L = lib()
@@ -643,6 +648,7 @@ def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: 
         check(L.nerf_march_macro(ptr(g), res, ptr(macro), s), "nerf_march_macro")
     packer.get(dtype_code(dtype), 0)  # (pack before the rounds)
     rounds = 0
+    live_hist = torch.zeros(64, dtype=torch.int32, device=dev)  # rays alive entering each round
     while True:
         # (the gather's int32 reservation counter: alive rays x K < 2^31)
         K = max(1, min(k_schedule[min(rounds, len(k_schedule) - 1)], cap, (2 ** 31 - 1) // max(N, 1)))
@@ -659,13 +665,17 @@ def march(packer: PackedMLP, rays: torch.Tensor, near: float, far: float, grid: 
         check(L.nerf_march_composite(ptr(raw), ptr(rays), N, ptr(t_table), ptr(off), ptr(cnt), ptr(out_step), ptr(T),
                                      ptr(rgb), ptr(depth), ptr(acc), ptr(nxt), ptr(alive), ptr(exh),
                                      float(step_size), float(t_thresh), stats.data_ptr(), s), "nerf_march_composite")
+        if rounds >= live_hist.numel():
+            live_hist = torch.cat([live_hist, torch.zeros_like(live_hist)])
+        live_hist[rounds:rounds + 1].copy_(counters[1:2])
         rounds += 1
         if rounds % sync_every == 0 and int(counters[1]) == 0:
             break
     check(L.nerf_march_finish(ptr(rgb), ptr(acc), N, int(bool(white_bkgd)), s), "nerf_march_finish")
     st = stats.tolist()
+    live_rounds = int((live_hist[:rounds] > 0).sum())
     return {"rgb_map_f": rgb, "depth_map_f": depth, "acc_map_f": acc, "n_queried": int(st[0]),
-            "n_evaluated": int(st[1]), "rounds": rounds}
+            "n_evaluated": int(st[1]), "rounds": live_rounds, "rounds_launched": rounds}
 
 
 # --------------------------------------------------------------------------------------

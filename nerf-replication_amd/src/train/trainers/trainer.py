@@ -54,6 +54,15 @@ class GradBuckets:
         self.works = []
         self.done = []
         self.packers = []
+        self.events = None  # a list: finish() appends (start, end) HIP events on the compute stream
+
+    def exposed_ms(self):
+        """Mean compute-stream time per step spent in finish() (waiting for the buckets + the
+        1/W scale): the part of the all-reduce the backward did not hide."""
+        if not self.events:
+            return None
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.events) / len(self.events)
 
     def attach(self, packers):
         self.packers = list(packers)
@@ -88,6 +97,10 @@ class GradBuckets:
         world = dist_world()
         if world == 1:
             return
+        ev = None
+        if self.events is not None and optimizer.flat_grad.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         for w in self.works:
             w.wait()
         g = optimizer.flat_grad
@@ -99,6 +112,9 @@ class GradBuckets:
                 dist.all_reduce(g[pos:off], op=dist.ReduceOp.SUM)
             pos = max(pos, off + n)
         g.mul_(1.0 / world)
+        if ev is not None:
+            ev[1].record()
+            self.events.append(ev)
         self.works, self.done = [], []
 
 

@@ -33,12 +33,37 @@ def interleaved_index(n: int, rank: int, world: int, block: int = RAY_BLOCK, dev
     return idx[idx < n]
 
 
+def ray_block(n: int, world: int, block: int = RAY_BLOCK) -> int:
+    """Rays per dealt block: ``block``, shrunk for small images so that every rank gets at
+    least one block whenever n >= world (a 40x40 view on 8 ranks: 200-ray blocks)."""
+    return max(1, min(block, -(-n // world)))
+
+
+def _meta(out, n_mine, keys):
+    """{key: ("ray", tail shape, dtype) | ("scalar", type name, None) | ("other", None, None)}
+    of a rank's render output, in the output's key order (the order every rank then walks the
+    keys in).  Per-ray tensors outside ``keys`` are dropped."""
+    m = {}
+    for k, v in out.items():
+        if torch.is_tensor(v) and v.dim() >= 1 and v.shape[0] == n_mine:
+            if keys is None or k in keys:
+                m[k] = ("ray", tuple(v.shape[1:]), v.dtype)
+        elif isinstance(v, (int, float)):
+            m[k] = ("scalar", type(v).__name__, None)
+        else:
+            m[k] = ("other", None, None)
+    return m
+
+
 def render_distributed(renderer, batch, accelerated: bool = False, keys=None, block: int = RAY_BLOCK):
     """Render batch['rays'] split across ranks; every rank returns the full outputs.
 
-    Rank r renders the rays of interleaved_index(n, r, W, block); per-ray outputs ([N] or
-    [N, c] tensors) are padded to the largest share, all_gathered and scattered back to ray
-    order; scalars (render_time, n_queried) are max- / sum-reduced."""
+    Rank r renders the rays of interleaved_index(n, r, W, ray_block(n, W, block)); per-ray
+    outputs ([N] or [N, c] tensors) are padded to the largest share, all_gathered and
+    scattered back to ray order; scalars (render_time, n_queried) are max- / sum-reduced.
+    Every rank issues the same collectives in the same order: a rank whose share is empty
+    (n < W) does not render, and the ranks first agree on the output keys (an object
+    all-gather, only in that case) so it joins every gather with a [0, ...] part."""
     world = _world()
     fn = renderer.render_accelerated if accelerated else renderer.render
     if world == 1:
@@ -47,19 +72,30 @@ def render_distributed(renderer, batch, accelerated: bool = False, keys=None, bl
     rays = batch["rays"]
     flat = rays.reshape(-1, 6)
     n = flat.shape[0]
-    idx = [interleaved_index(n, r, world, block, flat.device) for r in range(world)]
+    blk = ray_block(n, world, block)
+    idx = [interleaved_index(n, r, world, blk, flat.device) for r in range(world)]
     mine = idx[rank]
-    sub = dict(batch)
-    own = flat.index_select(0, mine)
-    sub["rays"] = own[None] if rays.dim() == 3 else own
-    out = fn(sub)
+    out = {}
+    if mine.numel() > 0:
+        sub = dict(batch)
+        own = flat.index_select(0, mine)
+        sub["rays"] = own[None] if rays.dim() == 3 else own
+        out = fn(sub)
+    meta = _meta(out, mine.numel(), keys)
+    if min(int(i.numel()) for i in idx) == 0:
+        metas = [None] * world
+        dist.all_gather_object(metas, meta)
+        meta = next((m for m in metas if m), {})
     share = max(int(i.numel()) for i in idx)
     res = {}
-    for k, v in out.items():
-        per_ray = torch.is_tensor(v) and v.dim() >= 1 and v.shape[0] == mine.numel()
-        if per_ray and keys is not None and k not in keys:
-            continue  # (keys selects the gathered per-ray outputs; scalars are always reduced)
-        if per_ray:
+    for k, (kind, info, dtype) in meta.items():
+        if k not in out:  # this rank rendered nothing
+            if kind == "ray":
+                out[k] = torch.zeros((0,) + info, dtype=dtype, device=flat.device)
+            elif kind == "scalar":
+                out[k] = 0 if info == "int" else 0.0
+        v = out.get(k)
+        if kind == "ray":
             pad = torch.zeros((share,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
             pad[: mine.numel()] = v
             parts = [torch.empty_like(pad) for _ in range(world)]

@@ -158,6 +158,75 @@ def test_interleaved_split_balances_a_central_workload():
     assert inter <= 1.02 and contig >= 2.0, (inter, contig)
 
 
+class _EmptyAwareRenderer(_FakeRenderer):
+    """As the reference Renderer.render: no rays -> {} (it must never be asked, though)."""
+
+    def render(self, batch):
+        r = batch["rays"].reshape(-1, 6)
+        if r.shape[0] == 0:
+            self.empty_calls = getattr(self, "empty_calls", 0) + 1
+            return {}
+        out = super().render(batch)
+        out["render_time"] = 0.5 + dist.get_rank()
+        return out
+
+    render_accelerated = render
+
+
+def _small_image_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      NERF_AMD_NO_ARGV="1")
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "nerf-replication_amd")]
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from src.utils.dist_render import render_distributed
+    results = []
+    # 2 rays on 3 ranks (one rank has nothing), 5 rays, a 40x40 view (< 256 * (W - 1) rays)
+    for n in (2, 5, 1600, 1001):
+        rays = torch.arange(n * 6, dtype=torch.float32).reshape(1, n, 6)
+        full = _FakeRenderer().render({"rays": rays})
+        fr = _EmptyAwareRenderer()
+        got = render_distributed(fr, {"rays": rays}, accelerated=(n == 5))
+        ok = all(torch.equal(got[k], full[k]) for k in ("rgb_map_f", "depth_map_f", "acc_map_f"))
+        ok = ok and got["n_queried"] == n and got["render_time"] == 0.5 + (world - 1 if n >= world else 1)
+        ok = ok and getattr(fr, "empty_calls", 0) == 0 and len(fr.seen) == (1 if (n >= world or rank < n) else 0)
+        results.append((n, ok))
+    q.put((rank, results))
+    dist.destroy_process_group()
+
+
+def test_small_image_split_no_rank_idle_and_no_deadlock():
+    """ADVICE r3: 256-ray blocks leave ranks without rays on images of <= 256 (W - 1) rays;
+    the reference renderer returns {} for zero rays and such a rank would skip the gathers the
+    others block in.  Blocks shrink so every rank renders when n >= W; when n < W the empty
+    rank skips rendering and joins the gathers with empty parts."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_small_image_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, results in res:
+        assert all(ok for _, ok in results), (rank, results)
+
+
+def test_ray_block_shrinks_for_small_images():
+    from src.utils.dist_render import RAY_BLOCK, interleaved_index, ray_block
+    assert ray_block(640000, 8) == RAY_BLOCK
+    for n, world in ((1600, 8), (7, 8), (8, 8), (2049, 8), (1, 1)):
+        b = ray_block(n, world)
+        idx = [interleaved_index(n, r, world, b) for r in range(world)]
+        assert torch.equal(torch.sort(torch.cat(idx)).values, torch.arange(n))
+        if n >= world:
+            assert min(i.numel() for i in idx) >= 1, (n, world, b)
+
+
 def _fake_bake_slab(res):
     """A deterministic 'bake' of voxel slab (x0, x1): cell (x, y, z) occupied iff (7x + 3y + z) % 5 == 0."""
     def f(slab):

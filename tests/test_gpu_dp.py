@@ -143,24 +143,34 @@ def test_two_rank_dp_step_matches_single_process(dtype):
 
 def test_prefetch_step_trains_like_the_plain_step(cuda):
     """Trainer.train_step(prefetch=...) enqueues the next batch's raygen + stratified sampling
-    before the optimizer update; with perturb 0 and the same ray stream it must give the same
-    parameters, bit for bit, as preparing each batch at the start of its own step."""
+    before the optimizer update.  With perturb 1 (training's default, where the stratified
+    jitter and the importance-sample uniforms come from the renderer's Philox stream) and the
+    same ray stream it must give the same losses and parameters, bit for bit, as the original
+    step with no preparation at all (to_cuda -> forward_backward -> apply): prefetching keeps
+    the per-step random stream."""
     runs = []
     for use_prefetch in (False, True):
         cfg, net, trainer, opt, ds, dev = _setup("fp32")
+        cfg.task_arg.perturb = 1
         losses = []
 
         def nxt():
             r, c = ds.sample_batch()
             return _batch(r, c, dev)
-        for step in range(3):
-            if use_prefetch:
-                batch = trainer.prefetched or trainer.prepare(nxt())
-                _, loss, _ = trainer.train_step(batch, opt, prefetch=nxt)
-                assert trainer.prefetched is not None and "_stratified0" in trainer.prefetched
-            else:
-                _, loss, _ = trainer.train_step(trainer.prepare(nxt()), opt)
-            losses.append(float(loss))
+        try:
+            for step in range(3):
+                if use_prefetch:
+                    batch = trainer.prefetched or trainer.prepare(nxt())
+                    _, loss, _ = trainer.train_step(batch, opt, prefetch=nxt)
+                    assert trainer.prefetched is not None and "_stratified0" in trainer.prefetched
+                else:
+                    batch = trainer.to_cuda(nxt())
+                    assert "_stratified0" not in batch
+                    _, loss, _ = trainer.forward_backward(batch, opt)
+                    trainer.apply(opt)
+                losses.append(float(loss))
+        finally:
+            cfg.task_arg.perturb = 0
         torch.cuda.synchronize()
         runs.append((losses, opt.flat_param.detach().cpu().clone()))
     assert runs[0][0] == runs[1][0]

@@ -496,13 +496,14 @@ def test_grid_index_bit_exact(golden, cuda, ops):
     np.testing.assert_array_equal(idx.cpu().numpy(), golden["grid_idx"])
 
 
-MARCH_CASES = [(d, r, m, True, False) for d in (0.02, 0.3, "blob") for r in (128, 512, 1024) for m in (True, False)]
-MARCH_CASES += [(d, 128, True, False, False) for d in (0.02, 0.3, "blob")]   # the two-pass form
-MARCH_CASES += [(d, 128, True, p, True) for d in (0.3, "blob") for p in (True, False)]  # buffer overflow
+MARCH_CASES = [(d, r, m, True, False, 6.0) for d in (0.02, 0.3, "blob") for r in (128, 512, 1024) for m in (True, False)]
+MARCH_CASES += [(d, 128, True, False, False, 6.0) for d in (0.02, 0.3, "blob")]   # the two-pass form
+MARCH_CASES += [(d, 128, True, p, True, 6.0) for d in (0.3, "blob") for p in (True, False)]  # buffer overflow
+MARCH_CASES += [(d, r, True, True, False, 24.0) for d in (0.3, "blob") for r in (128, 1024)]  # far bound > 8
 
 
-@pytest.mark.parametrize("density,res,macro,one_pass,tight", MARCH_CASES)
-def test_march_gather_empty_cell_skip_exact(cuda, ops, density, res, macro, one_pass, tight):
+@pytest.mark.parametrize("density,res,macro,one_pass,tight,far", MARCH_CASES)
+def test_march_gather_empty_cell_skip_exact(cuda, ops, density, res, macro, one_pass, tight, far):
     """The march gather skips the steps that provably stay in an empty cell (grid.hip,
     march_skip_empty).  Against brute force -- the occupancy of EVERY step's point o + t d
     (volume_renderer.py:298-309: clamp, normalise, x127, truncate) -- the one-round gather with
@@ -514,7 +515,9 @@ def test_march_gather_empty_cell_skip_exact(cuda, ops, density, res, macro, one_
     one-pass form writes the points from the runs its counting walk recorded (16 per lane, then
     the walk again: the dense grids' rays have far more runs) and must equal the two-pass form;
     'tight' gives the round half the room it needs: every reserved position below cap holds its
-    ray's next occupied step, the overflowing rays keep their start step and gather again."""
+    ray's next occupied step, the overflowing rays keep their start step and gather again.
+    far = 24: a t table past 8, origins ~12 out and |d| = 0.5, so |t d| ~ 12 at the
+    box: the skip margin's absolute floor must grow with the table's largest t."""
     from nerf_amd._lib import lib, ptr, stream_of
     g = torch.Generator().manual_seed(31)
     N = 3000
@@ -533,10 +536,14 @@ def test_march_gather_empty_cell_skip_exact(cuda, ops, density, res, macro, one_
                    torch.rand(N - N // 2, 3, generator=g) * 2 - 1])
     tgt = torch.rand(N, 3, generator=g) * 2.4 - 1.2
     d = tgt - o
+    if far > 8.0:
+        o[: N // 2] += torch.tensor([0.0, 0.0, 8.0])
+        d = tgt - o
+        d = d / d.norm(dim=1, keepdim=True) * 0.5
     d[::7, 0] = 0.0                                   # axis-aligned components
     d[::11, 1] = 0.0
     rays = torch.cat([o, d], 1).float().to(cuda).contiguous()
-    t_table = ops.device_table("arange", 2.0, 6.0, 0.005, cuda)
+    t_table = ops.device_table("arange", 2.0, far, 0.005, cuda)
     S = t_table.numel()
     # brute force: every step's point, the lookup of grid_index
     pts = rays[:, None, :3] + t_table[None, :, None] * rays[:, None, 3:]
