@@ -13,9 +13,10 @@ Weights: the reference's seed-0 init (torch.manual_seed(0); Network()).  Data is
 synthetic (no dataset offline).  Rank 0 prints one JSON line.
 
 The headline (``value``, ``dtype`` "fp32") runs the MLP in fp32 MFMA, the reference's own
-precision (nn.Linear fp32, network.py:22-74).  Two opt-in MLP precisions are measured in the
+precision (nn.Linear fp32, network.py:22-74).  Three opt-in MLP precisions are measured in the
 same run and reported as nested, labelled lines: ``bf16x3_line`` (split-bf16 operands, three
-bf16 MFMAs per product, ~1e-5 relative per dot product; priced against 1/3 of the bf16 peak)
+bf16 MFMAs per product, ~1e-5 relative per dot product; priced against 1/3 of the bf16 peak),
+``bf16x3f_line`` (the bf16x3 forward -- its rgb/depth are bf16x3's -- with the bf16 backward)
 and ``bf16_line`` (north_star: rgb/depth within 2e-3).
 ``vs_baseline`` divides by the reference's per-step op graph run eagerly by PyTorch-ROCm on
 the same GPU at the same MLP dtype and perturb (``baseline``); ``cpu_baseline`` is the same
@@ -51,6 +52,16 @@ MLP_IO_BYTES = 12 + 16 + 16
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 # MI355X dense MFMA (MI355X_MICROARCH.md); bf16x3 spends 3 bf16 MFMAs per fp32 product
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3}
+ALL_DTYPES = ("fp32", "bf16x3", "bf16x3f", "bf16")
+
+
+def kernel_prec(kernel: str, dtype: str) -> str:
+    """The arithmetic a kernel of an MLP tier runs in: bf16x3f = bf16x3 forward + bf16 backward."""
+    if dtype == "bf16x3f":
+        return "bf16x3" if kernel.startswith("mlp_fwd") else "bf16"
+    return dtype
+
+
 # HBM-bound sampling / compositing kernels; ops.py counts their algorithmic bytes per launch
 STREAM_KERNELS = ("raygen", "sample_stratified", "sample_pdf", "composite_fwd", "composite_bwd")
 
@@ -63,7 +74,7 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU per step")
-    ap.add_argument("--dtype", default="fp32", choices=["bf16", "bf16x3", "fp32"], help="headline MLP dtype")
+    ap.add_argument("--dtype", default="fp32", choices=list(ALL_DTYPES), help="headline MLP dtype")
     ap.add_argument("--images", type=int, default=100)
     ap.add_argument("--res", type=int, default=800)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -251,8 +262,9 @@ def mlp_roofline(k, n, ms, units, dtype):
     avg_ms = ms / n
     per = FLOP_PER_SAMPLE[k] * units / n
     ach = per / (avg_ms * 1e-3) / 1e12
-    return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s",
-            "frac": round(ach / PEAK_TFLOPS[dtype], 4), "flop_per_launch": per, "samples_per_launch": units // n,
+    peak = PEAK_TFLOPS[kernel_prec(k, dtype)]
+    return {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "flop_per_launch": per, "samples_per_launch": units // n,
             "avg_launch_ms": round(avg_ms, 4)}
 
 
@@ -311,7 +323,7 @@ def measure_training(args, world, rank, device, dtype):
     value = world * args.rays * args.steps / elapsed
     # dominant kernel: largest total device time among the MLP kernels
     name, (n_launch, ms, units) = max(ktimes.items(), key=lambda kv: kv[1][1])
-    esize = 2 if dtype == "bf16" else 4
+    esize = 2 if dtype in ("bf16", "bf16x3f") else 4
     traffic, traffic_src = pmc_traffic(name, dtype)
     store_bytes = STORE_ROWS * esize * units / n_launch
     io_bytes = MLP_IO_BYTES * units / n_launch
@@ -616,7 +628,7 @@ def main():
     if want > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(want, sys.argv[1:]))
     world, rank, device = setup_dist()
-    others = [] if args.no_second else [d for d in ("fp32", "bf16x3", "bf16") if d != args.dtype]
+    others = [] if args.no_second else [d for d in ALL_DTYPES if d != args.dtype]
     lines = {}
     for dtype in [args.dtype] + others:
         log(f"training {dtype}: {args.warmup} warmup + {args.steps} timed steps")
@@ -632,7 +644,7 @@ def main():
         eager = None
         if rank == 0 and world == 1 and not args.no_eager_baseline:
             # bf16x3 stands in for fp32 arithmetic: its baseline is the reference's fp32 eager step
-            eager = eager_gpu_baseline(device, args.rays, "fp32" if dtype == "bf16x3" else dtype)
+            eager = eager_gpu_baseline(device, args.rays, "fp32" if dtype in ("bf16x3", "bf16x3f") else dtype)
             log(f"{dtype}: eager PyTorch-ROCm {eager['value']} rays/s")
         lines[dtype] = {
             "value": round(value, 1), "ms_per_step": round(ms_step, 3), "dtype": dtype,

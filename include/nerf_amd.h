@@ -96,7 +96,10 @@ int nerf_composite_bwd(const float* raw, const float* z, const float* dirs, int 
  * act / masks / dz are opaque workspaces of nerf_mlp_{act,mask,dz}_bytes(M) bytes written by the
  * training forward (flags & NERF_MLP_STORE) and the dX chain; their layouts are internal.
  * dtype: 0 = fp32 (fp32 MFMA, the reference's precision), 1 = bf16 (operands rounded to bf16),
- * 2 = bf16x3 (operands split into bf16 hi + lo, three bf16 MFMAs per product, fp32 accumulation). */
+ * 2 = bf16x3 (operands split into bf16 hi + lo, three bf16 MFMAs per product, fp32 accumulation),
+ * 3 = bf16x3f: the bf16x3 forward (its outputs are bf16x3's, bit for bit) whose training stores are
+ * the bf16 (hi) halves, and the bf16 backward (dX chain, dW).  Every function maps 3 to its part:
+ * packed_bytes / pack dir 0 and fwd -> bf16x3, pack dir 1 / act / dz bytes / bwd -> bf16. */
 int64_t nerf_mlp_net_params(void);
 int64_t nerf_mlp_param_offset(int i);
 int64_t nerf_mlp_packed_bytes(int dtype, int dir);

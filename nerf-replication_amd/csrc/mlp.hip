@@ -686,11 +686,13 @@ __device__ __forceinline__ void store16(uint4* p, uint4 v) {
     p[OFF / 16] = v;
   }
 }
-template <class P>
+// SCH: chunks stored per tile (P::CH; 2 for a bf16x3 tile stored as its bf16 hi half, the
+// bf16 tile-block layout)
+template <class P, int SCH = P::CH>
 __device__ __forceinline__ void store_tile(void* base, int64_t nblk, int ntiles, int tau, int64_t wblock, int lane,
                                            const typename P::Tile& t) {
-  uint4* dst = (uint4*)base + tile_kib(nblk, ntiles, tau, wblock, 0, P::CH) * 64 + lane;
-  sfor<P::CH>([&](auto cc) {
+  uint4* dst = (uint4*)base + tile_kib(nblk, ntiles, tau, wblock, 0, SCH) * 64 + lane;
+  sfor<SCH>([&](auto cc) {
     constexpr int c = decltype(cc)::value;
     store16<c * 1024>(dst, P::chunk(t, c));
   });
@@ -724,10 +726,15 @@ struct FwdArgs {
   int64_t M_cap;
 };
 
-template <class P, bool STORE, bool DENSITY, bool PERSIST = false>
+// HALF (bf16x3 only): the training stores keep each tile's bf16 hi half in the bf16 layout
+// (2 chunks per tile-block) for a bf16 backward -- the "bf16x3f" tier: bf16x3 outputs, bf16
+// gradients.  hi = RNE bf16 of the fp32-class value, exactly what a bf16 forward stores.
+template <class P, bool STORE, bool DENSITY, bool PERSIST = false, bool HALF = false>
 struct FwdWave {
   using Tile = typename P::Tile;
   static constexpr int CH = P::CH;
+  static_assert(!HALF || (P::KIND == K_BF16X3 && STORE), "half stores: bf16x3 training forward only");
+  static constexpr int SCH = HALF ? 2 : P::CH;  // chunks stored per tile
   using GT = GroupTable<0, DENSITY, P::CH>;
 
   const FwdArgs& a;
@@ -778,9 +785,9 @@ struct FwdWave {
   static __host__ __device__ constexpr int unit_stores(int u) {
     if (!STORE) return 0;
     const int L = fwd_unit_layer(u), n = u - fwd_unit_first(L);
-    if (L == LFA) return n < 8 ? CH : 0;
+    if (L == LFA) return n < 8 ? SCH : 0;
     if (L == LRGB) return 0;
-    return CH + (n == fwd_out_tiles(L) - 1 ? 1 : 0);  // + the layer's mask store
+    return SCH + (n == fwd_out_tiles(L) - 1 ? 1 : 0);  // + the layer's mask store
   }
   static __host__ __device__ constexpr int group_stores(int g) {
     int s = 0;
@@ -825,7 +832,7 @@ struct FwdWave {
       }
       out_arr<L>()[n] = out;
       if constexpr (STORE) {
-        store_tile<P>(a.act, a.nblk, AT_TILES, (L == LV ? AT_V : AT_H + 8 * L) + n, wblock, lane, out);
+        store_tile<P, SCH>(a.act, a.nblk, AT_TILES, (L == LV ? AT_V : AT_H + 8 * L) + n, wblock, lane, out);
         if constexpr ((n & 1) == 0) mw[n >> 1] = bits;
         else mw[n >> 1] |= bits << 8;
         if constexpr (n == fwd_out_tiles(L) - 1)
@@ -853,7 +860,7 @@ struct FwdWave {
           }
         }
         Ha[n] = out;
-        if constexpr (STORE) store_tile<P>(a.act, a.nblk, AT_TILES, AT_F + n, wblock, lane, out);
+        if constexpr (STORE) store_tile<P, SCH>(a.act, a.nblk, AT_TILES, AT_F + n, wblock, lane, out);
       } else {
         alpha = acc[0];  // alpha_linear: output row 0 = register 0 of lanes 0..31
       }
@@ -916,7 +923,7 @@ struct FwdWave {
     wb = lds_ptr(slot + (uint32_t)(h * 16));
     group_body<P, 0, DENSITY, g>(*this, lds_ptr(slot + (uint32_t)(lane * 16)));
     constexpr int N = handoff_vmcnt<P, 0, DENSITY>(g, [](int i) constexpr { return group_stores(i); },
-                                                   STORE ? 3 * CH : 0);
+                                                   STORE ? 3 * SCH : 0);
     if constexpr (g + 1 < NG) wait_barrier<N>();
   }
 
@@ -938,13 +945,13 @@ struct FwdWave {
     if constexpr (STORE) {
       Tile Dt;
       pe_tile<P, 0, 4, 27>(Dt, h, dx, dy, dz);
-      store_tile<P>(a.act, a.nblk, AT_TILES, AT_X, wblock, lane, X[0]);
-      store_tile<P>(a.act, a.nblk, AT_TILES, AT_X + 1, wblock, lane, X[1]);
-      store_tile<P>(a.act, a.nblk, AT_TILES, AT_D, wblock, lane, Dt);
+      store_tile<P, SCH>(a.act, a.nblk, AT_TILES, AT_X, wblock, lane, X[0]);
+      store_tile<P, SCH>(a.act, a.nblk, AT_TILES, AT_X + 1, wblock, lane, X[1]);
+      store_tile<P, SCH>(a.act, a.nblk, AT_TILES, AT_D, wblock, lane, Dt);
     }
     {  // group 0 landed: younger = the DMAs of groups 1 .. PF - 1 and the PE stores
       constexpr int N0 = [] {
-        int n = STORE ? 3 * CH : 0;
+        int n = STORE ? 3 * SCH : 0;
         for (int j = 1; j < PF && j < GT::t.n; ++j) n += group_dma<P, 0, DENSITY>(j);
         return n;
       }();
@@ -972,12 +979,12 @@ __device__ __forceinline__ void young_priority() {
 // march's gather count: no host round trip sizes the launch) and a grid of one wave of
 // workgroups loops over the sample blocks; the barrier at the end of each block keeps the next
 // block's prologue DMA out of the ring slot still being read.
-template <class P, bool STORE, bool DENSITY, bool PERSIST>
+template <class P, bool STORE, bool DENSITY, bool PERSIST, bool HALF = false>
 __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
   young_priority();
   if constexpr (!PERSIST) {
-    FwdWave<P, STORE, DENSITY> w(a, smem_u4, blockIdx.x, threadIdx.x);
+    FwdWave<P, STORE, DENSITY, false, HALF> w(a, smem_u4, blockIdx.x, threadIdx.x);
     w.run();
   } else {
     static_assert(!STORE, "the persistent forward is inference only");
@@ -1814,14 +1821,14 @@ static void allow_lds(K kernel, size_t bytes) {
   if (bytes > 65536) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
-template <class P, bool STORE, bool DENSITY>
+template <class P, bool STORE, bool DENSITY, bool HALF = false>
 static void launch_fwd(const FwdArgs& a, hipStream_t stream) {
-  static const bool lds_ok = (allow_lds(fwd_kernel<P, STORE, DENSITY, false>, fwd_lds_bytes<P>()), true);
+  static const bool lds_ok = (allow_lds(fwd_kernel<P, STORE, DENSITY, false, HALF>, fwd_lds_bytes<P>()), true);
   (void)lds_ok;
   const int spb = samples_per_block<P>();
   dim3 grid((unsigned)(STORE ? a.nblk * 32 / spb : (a.M + spb - 1) / spb));
-  hipLaunchKernelGGL((fwd_kernel<P, STORE, DENSITY, false>), grid, dim3(P::WAVES * 64), fwd_lds_bytes<P>(), stream,
-                     a);
+  hipLaunchKernelGGL((fwd_kernel<P, STORE, DENSITY, false, HALF>), grid, dim3(P::WAVES * 64), fwd_lds_bytes<P>(),
+                     stream, a);
 }
 
 // persistent inference forward: one wave of workgroups (every CU x its resident workgroups),
@@ -1876,6 +1883,11 @@ template <class P>
 void mlp_fwd_train_impl(const FwdArgs& a, hipStream_t stream) {
   launch_fwd<P, true, false>(a, stream);
 }
+// bf16x3 forward, bf16 (hi-half) stores for the bf16 backward
+void mlp_fwd_train_half_impl(const FwdArgs& a, hipStream_t stream);
+#if defined(NERF_MLP_PREC) && NERF_MLP_PREC == 2 && (!defined(NERF_MLP_PART) || NERF_MLP_PART == 4)
+void mlp_fwd_train_half_impl(const FwdArgs& a, hipStream_t stream) { launch_fwd<PBF3, true, false, true>(a, stream); }
+#endif
 template <class P>
 void mlp_fwd_infer_impl(const FwdArgs& a, bool density, hipStream_t stream) {
   if (a.M_dev) launch_fwd_persist<P>(a, stream);
@@ -1937,24 +1949,31 @@ extern "C" {
 int64_t nerf_mlp_net_params(void) { return NET_PARAMS; }
 int64_t nerf_mlp_param_offset(int i) { return (i >= 0 && i <= NPARAM) ? param_offset(i) : -1; }
 
+// dtype 3 (bf16x3f) = a bf16x3 forward (its forward pack) whose training stores are bf16, with
+// the bf16 backward (its W^T pack, bf16 dZ): every function below maps it to its part
+static int fwd_prec(int dtype) { return dtype == 3 ? 2 : dtype; }
+static int bwd_prec(int dtype) { return dtype == 3 ? 1 : dtype; }
+static int store_prec(int dtype) { return dtype == 3 ? 1 : dtype; }
+
 int64_t nerf_mlp_packed_bytes(int dtype, int dir) {
-  if (dtype < 0 || dtype > 2 || (dir != 0 && dir != 1)) return -1;
-  return total_chunks(dtype == 1 ? PBF16::CH : PF32::CH, dir) * 1024;  // bf16x3: CH 4 as fp32
+  if (dtype < 0 || dtype > 3 || (dir != 0 && dir != 1)) return -1;
+  const int p = dir == 0 ? fwd_prec(dtype) : bwd_prec(dtype);
+  return total_chunks(p == 1 ? PBF16::CH : PF32::CH, dir) * 1024;  // bf16x3: CH 4 as fp32
 }
 
 int64_t nerf_mlp_padded_samples(int64_t M) { return (M + M_ALIGN - 1) / M_ALIGN * M_ALIGN; }
 int64_t nerf_mlp_act_bytes(int dtype, int64_t M) {
-  return (int64_t)A_ROWS * nerf_mlp_padded_samples(M) * (dtype == 1 ? 2 : 4);
+  return (int64_t)A_ROWS * nerf_mlp_padded_samples(M) * (store_prec(dtype) == 1 ? 2 : 4);
 }
 int64_t nerf_mlp_dz_bytes(int dtype, int64_t M) {
-  return (int64_t)Z_ROWS * nerf_mlp_padded_samples(M) * (dtype == 1 ? 2 : 4);
+  return (int64_t)Z_ROWS * nerf_mlp_padded_samples(M) * (store_prec(dtype) == 1 ? 2 : 4);
 }
 int64_t nerf_mlp_mask_bytes(int64_t M) { return nerf_mlp_padded_samples(M) / 32 * MASK_GROUPS * 64 * 16; }
 
 int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void* packed_bwd, hipStream_t stream) {
   NERF_REQUIRE(params != nullptr, "nerf_mlp_pack: params is null");
-  NERF_REQUIRE(dtype >= 0 && dtype <= 2, "nerf_mlp_pack: dtype must be 0 (f32), 1 (bf16) or 2 (bf16x3), got %d",
-               dtype);
+  NERF_REQUIRE(dtype >= 0 && dtype <= 3,
+               "nerf_mlp_pack: dtype must be 0 (f32), 1 (bf16), 2 (bf16x3) or 3 (bf16x3f), got %d", dtype);
   ParamPtrs prm;
   for (int i = 0; i < NPARAM; ++i) {
     NERF_REQUIRE(params[i] != nullptr, "nerf_mlp_pack: params[%d] is null", i);
@@ -1963,8 +1982,9 @@ int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void*
   for (int dir = 0; dir < 2; ++dir) {
     void* dst = dir == 0 ? packed_fwd : packed_bwd;
     if (!dst) continue;
-    if (dtype == 0) mlp_pack_impl<PF32>(prm, dir, (char*)dst, stream);
-    else if (dtype == 1) mlp_pack_impl<PBF16>(prm, dir, (char*)dst, stream);
+    const int p = dir == 0 ? fwd_prec(dtype) : bwd_prec(dtype);
+    if (p == 0) mlp_pack_impl<PF32>(prm, dir, (char*)dst, stream);
+    else if (p == 1) mlp_pack_impl<PBF16>(prm, dir, (char*)dst, stream);
     else mlp_pack_impl<PBF3>(prm, dir, (char*)dst, stream);
     if (int e = check_launch("nerf_mlp_pack")) return e;
   }
@@ -1975,7 +1995,7 @@ int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void*
 int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const float* viewdirs, int samples_per_dir,
                  const int32_t* dir_index, int64_t M, int flags, float* raw, void* act, uint16_t* masks,
                  hipStream_t stream) {
-  NERF_REQUIRE(dtype >= 0 && dtype <= 2, "nerf_mlp_fwd: bad dtype %d", dtype);
+  NERF_REQUIRE(dtype >= 0 && dtype <= 3, "nerf_mlp_fwd: bad dtype %d", dtype);
   NERF_REQUIRE(M >= 0, "nerf_mlp_fwd: M < 0");
   if (M == 0) return 0;
   const bool store = flags & 1, density = flags & 2;
@@ -1989,7 +2009,8 @@ int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const floa
   if (store) {
     if (dtype == 0) mlp_fwd_train_impl<PF32>(a, stream);
     else if (dtype == 1) mlp_fwd_train_impl<PBF16>(a, stream);
-    else mlp_fwd_train_impl<PBF3>(a, stream);
+    else if (dtype == 2) mlp_fwd_train_impl<PBF3>(a, stream);
+    else mlp_fwd_train_half_impl(a, stream);
   } else {
     if (dtype == 0) mlp_fwd_infer_impl<PF32>(a, density, stream);
     else if (dtype == 1) mlp_fwd_infer_impl<PBF16>(a, density, stream);
@@ -2002,7 +2023,7 @@ int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const floa
 // the launch (the grid march's rounds)
 int nerf_mlp_fwd_count(const void* packed_fwd, int dtype, const float* pts, const float* viewdirs, int samples_per_dir,
                        const int32_t* dir_index, const int32_t* M_dev, int64_t M_cap, float* raw, hipStream_t stream) {
-  NERF_REQUIRE(dtype >= 0 && dtype <= 2, "nerf_mlp_fwd_count: bad dtype %d", dtype);
+  NERF_REQUIRE(dtype >= 0 && dtype <= 3, "nerf_mlp_fwd_count: bad dtype %d", dtype);
   NERF_REQUIRE(M_cap >= 0, "nerf_mlp_fwd_count: M_cap < 0");
   if (M_cap == 0) return 0;
   NERF_REQUIRE(packed_fwd && pts && raw && viewdirs && M_dev, "nerf_mlp_fwd_count: null pointer");
@@ -2116,14 +2137,15 @@ static void dw_items(int dtype, int64_t nblk, int item_off[NDWJOB + 1], int job_
 }
 int64_t nerf_mlp_dw_items(int dtype, int64_t M) {
   int off[NDWJOB + 1], job[NDWJOB];
-  dw_items(dtype, nerf_mlp_padded_samples(M) / 32, off, job);
+  dw_items(bwd_prec(dtype), nerf_mlp_padded_samples(M) / 32, off, job);
   return off[NDWJOB];
 }
 
 // dX chain only: dz (per-layer output gradients, fragment-native tiles) from d_raw + masks
 int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64_t M, const uint16_t* masks, void* dz,
                     hipStream_t stream) {
-  NERF_REQUIRE(dtype >= 0 && dtype <= 2, "nerf_mlp_bwd_dx: bad dtype %d", dtype);
+  NERF_REQUIRE(dtype >= 0 && dtype <= 3, "nerf_mlp_bwd_dx: bad dtype %d", dtype);
+  dtype = bwd_prec(dtype);
   NERF_REQUIRE(M >= 0, "nerf_mlp_bwd_dx: M < 0");
   if (M == 0) return 0;
   NERF_REQUIRE(packed_bwd && d_raw && masks && dz, "nerf_mlp_bwd_dx: null pointer");
@@ -2144,7 +2166,8 @@ int64_t nerf_mlp_dw_workspace_bytes(int dtype, int64_t M) {
 // null: fp32 atomics.
 int nerf_mlp_bwd_dw_ws(int dtype, int64_t M, const void* act, const void* dz, float* grad, void* workspace,
                        hipStream_t stream) {
-  NERF_REQUIRE(dtype >= 0 && dtype <= 2, "nerf_mlp_bwd_dw: bad dtype %d", dtype);
+  NERF_REQUIRE(dtype >= 0 && dtype <= 3, "nerf_mlp_bwd_dw: bad dtype %d", dtype);
+  dtype = bwd_prec(dtype);
   NERF_REQUIRE(M >= 0, "nerf_mlp_bwd_dw: M < 0");
   if (M == 0) return 0;
   NERF_REQUIRE(act && dz && grad, "nerf_mlp_bwd_dw: null pointer");

@@ -22,10 +22,22 @@ import torch
 
 from ._lib import check, lib, ptr, stream_of
 
-F32, BF16, BF16X3 = 0, 1, 2
+F32, BF16, BF16X3, BF16X3F = 0, 1, 2, 3
 # bf16x3: fp32 operands split into bf16 hi + lo, products hi*hi + hi*lo + lo*hi on the bf16
-# MFMA with fp32 accumulation (csrc/mlp.hip PBF3): fp32-class results at bf16-MFMA cost x3
-DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16, "bf16x3": BF16X3}
+# MFMA with fp32 accumulation (csrc/mlp.hip PBF3): fp32-class results at bf16-MFMA cost x3.
+# bf16x3f: the bf16x3 forward (outputs identical to bf16x3's) with the bf16 backward (its
+# training stores are the bf16 hi halves): bf16x3 outputs, bf16 gradients
+DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16, "bf16x3": BF16X3,
+          "bf16x3f": BF16X3F}
+DTYPE_NAMES = {F32: "fp32", BF16: "bf16", BF16X3: "bf16x3", BF16X3F: "bf16x3f"}
+
+
+def pack_code(dtype: int, direction: int) -> int:
+    """The packed-weight layout a (dtype, direction) uses: bf16x3f packs its forward as
+    bf16x3 and its backward (W^T) as bf16, so it shares those caches."""
+    if dtype == BF16X3F:
+        return BF16X3 if direction == 0 else BF16
+    return dtype
 
 SCENE_BBOX = ((-1.5, -1.5, -1.5), (1.5, 1.5, 1.5))
 
@@ -34,7 +46,7 @@ def dtype_code(d) -> int:
     if isinstance(d, int):
         return d
     if d not in DTYPES:
-        raise ValueError(f"unsupported MLP dtype {d!r} (fp32, bf16 or bf16x3)")
+        raise ValueError(f"unsupported MLP dtype {d!r} (fp32, bf16, bf16x3 or bf16x3f)")
     return DTYPES[d]
 
 
@@ -391,6 +403,7 @@ class PackedMLP:
         return (_PARAM_GENERATION[0],) + tuple((p.data_ptr(), p._version) for p in self.params)
 
     def get(self, dtype: int, direction: int) -> torch.Tensor:
+        dtype = pack_code(dtype, direction)
         key = self._key()
         ent = self._cache.get((dtype, direction))
         if ent is not None and ent[0] == key:

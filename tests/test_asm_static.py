@@ -24,6 +24,8 @@ def test_mlp_kernels_handoffs_and_registers(capsys):
     kernels = ["fwd_kernel<nerf::mlp::PBF16, true, false, false>", "dx_kernel<nerf::mlp::PBF16>", "dw_kernel<nerf::mlp::PBF16>",
                "fwd_kernel<nerf::mlp::PF32, true, false, false>", "dx_kernel<nerf::mlp::PF32>", "dw_kernel<nerf::mlp::PF32>",
                "fwd_kernel<nerf::mlp::PBF3, true, false, false>", "dx_kernel<nerf::mlp::PBF3>", "dw_kernel<nerf::mlp::PBF3>",
+               # bf16x3f: the bf16x3 training forward storing bf16 halves
+               "fwd_kernel<nerf::mlp::PBF3, true, false, false, true>",
                # the persistent inference forwards of the grid march (device-side sample count)
                "fwd_kernel<nerf::mlp::PF32, false, false, true>", "fwd_kernel<nerf::mlp::PBF16, false, false, true>"]
     with tempfile.TemporaryDirectory() as tmp:
@@ -36,10 +38,11 @@ def test_mlp_kernels_handoffs_and_registers(capsys):
     for m in re.finditer(r"BAD scratch (\d+) B in (\S+)", out):
         # the persistent inference forwards (PERSIST = true) re-run the straight-line body per sample
         # block: a few hundred bytes of spills, reloaded ~70 times per block of ~40k instructions
-        persist = re.search(r"Lb0ELb0ELb1E", m.group(2)) is not None
+        persist = re.search(r"Lb0ELb0ELb1ELb0EE", m.group(2)) is not None
         assert (("fwd_kernelINS0_4PF32ELb1ELb0" in m.group(2) and int(m.group(1)) <= 24)
                 or (persist and int(m.group(1)) <= 320)), "\n" + out
     assert re.search(r"ok  _ZN4nerf3mlp10fwd_kernelINS0_5PBF16ELb0ELb0ELb1E", out), "\n" + out
     for name in ("fwd_kernelINS0_5PBF16ELb1ELb0", "fwd_kernelINS0_4PF32ELb1ELb0", "dx_kernelINS0_4PF32",
-                 "fwd_kernelINS0_4PBF3ELb1ELb0", "dx_kernelINS0_4PBF3"):
+                 "fwd_kernelINS0_4PBF3ELb1ELb0ELb0ELb0E", "dx_kernelINS0_4PBF3",
+                 "fwd_kernelINS0_4PBF3ELb1ELb0ELb0ELb1E"):
         assert re.search(name + r".*counted_waits=\d+ unsafe=0", out), "\n" + out

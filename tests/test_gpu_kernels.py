@@ -378,36 +378,42 @@ def test_pe_fused_tiles(cuda, ops, O, seeded_state, dtype):
 BF16_EMU_TOL = 3e-3
 
 
-def _bf16_emulated_mlp(p, x63, d27, mk, gout):
+def _bf16_emulated_mlp(p, x63, d27, mk, gout, fwd_exact=False):
     """The bf16 kernels' arithmetic in fp64 (csrc/mlp.hip PBF16): every MFMA operand rounded to
     bf16 (RNE) where the kernel rounds it -- the PE tiles, the weights (fwd W, dX W^T), each
     layer's post-ReLU activation and the feature output, the output gradients d rgb / d alpha and
     each stage's masked pre-activation gradient dZ -- with the bias as the fp32 initial
     accumulator, the kernel's own ReLU masks ``mk`` and exact (fp64) accumulation.  Returns (raw,
-    {param: grad}); dW = sum_m bf16(dZ) bf16(act), db = sum_m bf16(dZ)."""
+    {param: grad}); dW = sum_m bf16(dZ) bf16(act), db = sum_m bf16(dZ).
+    fwd_exact (bf16x3f): the forward is exact (fp64, fp32-class weights and activations, as the
+    bf16x3 forward computes it) and only what it STORES for the backward is rounded to bf16 --
+    the activations, the PE tiles -- while the backward is the bf16 one (bf16 W^T, bf16 dZ)."""
     bf = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
+    fr = (lambda t: t) if fwd_exact else bf  # rounding inside the forward  # noqa: E731
     hm = lambda tile0, n: torch.cat([mk[tile0 + j] for j in range(n)], 1).double()  # noqa: E731
     W = {k: bf(w.double()) for k, (w, b) in p.items()}
+    Wf = {k: fr(w.double()) for k, (w, b) in p.items()}
     B = {k: b.double() for k, (w, b) in p.items()}
-    xb, db_ = bf(x63), bf(d27)
+    xf, df_ = fr(x63.double()), fr(d27.double())
     ins, masks = [], []
-    h = xb
+    h = xf
     for i in range(8):
         n = f"pts_linears.{i}"
-        ins.append(h)
+        ins.append(bf(h))
         m = hm(8 * i, 8)
         masks.append(m)
-        h = bf((h @ W[n].t() + B[n]) * m)
+        h = fr((h @ Wf[n].t() + B[n]) * m)
         if i == 4:
-            h = torch.cat([xb, h], -1)
+            h = torch.cat([xf, h], -1)
     h7 = h
-    alpha = h7 @ W["alpha_linear"].t() + B["alpha_linear"]
-    feat = bf(h7 @ W["feature_linear"].t() + B["feature_linear"])
-    vin = torch.cat([feat, db_], -1)
+    alpha = h7 @ Wf["alpha_linear"].t() + B["alpha_linear"]
+    feat = fr(h7 @ Wf["feature_linear"].t() + B["feature_linear"])
+    vin_f = torch.cat([feat, df_], -1)
     mv = hm(64, 4)
-    hv = bf((vin @ W["views_linears.0"].t() + B["views_linears.0"]) * mv)
-    rgb = hv @ W["rgb_linear"].t() + B["rgb_linear"]
+    hv_f = fr((vin_f @ Wf["views_linears.0"].t() + B["views_linears.0"]) * mv)
+    rgb = hv_f @ Wf["rgb_linear"].t() + B["rgb_linear"]
     raw = torch.cat([rgb, alpha], -1)
+    h7, vin, hv = bf(h7), bf(vin_f), bf(hv_f)
     g = {}
     g_rgb, g_a = bf(gout[:, :3].double()), bf(gout[:, 3:].double())
 
@@ -431,7 +437,8 @@ def _bf16_emulated_mlp(p, x63, d27, mk, gout):
     return raw, g
 
 
-@pytest.mark.parametrize("dtype,M", [("fp32", 20010), ("bf16x3", 20010), ("bf16", 20010), ("bf16", 131101)])
+@pytest.mark.parametrize("dtype,M", [("fp32", 20010), ("bf16x3", 20010), ("bf16", 20010), ("bf16", 131101),
+                                     ("bf16x3f", 20010)])
 def test_mlp_backward_kernel_masks(cuda, ops, O, seeded_state, dtype, M):
     """Many dW sample chunks (the last partial) and a ragged final block, against an fp64
     oracle that takes the kernel's own ReLU masks: at these sizes a few pre-activations sit
@@ -440,7 +447,9 @@ def test_mlp_backward_kernel_masks(cuda, ops, O, seeded_state, dtype, M):
     fp32 and bf16x3 (16-bit split operands; measured <= 1.7e-5): 1e-4 of the largest entry.
     bf16: against the fp64 emulation of its own rounding (_bf16_emulated_mlp), raw and every
     gradient entry within BF16_EMU_TOL of the largest: what remains is fp32 accumulation order
-    and the rare operand that sits within fp32 error of a bf16 rounding boundary."""
+    and the rare operand that sits within fp32 error of a bf16 rounding boundary.
+    bf16x3f (bf16x3 forward, bf16 backward on the forward's bf16-rounded stores): raw within 1e-4
+    of the exact forward, every gradient entry within BF16_EMU_TOL of its rounding model."""
     from nerf_amd._lib import lib, ptr, stream_of
     g = torch.Generator().manual_seed(12)
     spd = 10
@@ -464,11 +473,13 @@ def test_mlp_backward_kernel_masks(cuda, ops, O, seeded_state, dtype, M):
 
     dirs = vd[:, None].expand(-1, spd, 3).reshape(-1, 3)[:M]
     errs = {}
-    if dtype == "bf16":
+    if dtype in ("bf16", "bf16x3f"):
         emb = torch.cat([O.positional_encoding(pts, 10), O.positional_encoding(dirs, 4)], -1)
         sp = O.split_params({k: v for k, v in seeded_state.items() if k.startswith("model.")}, "model")
-        ref_raw, ref_g = _bf16_emulated_mlp(sp, emb[:, :63], emb[:, 63:], mk, gout)
+        ref_raw, ref_g = _bf16_emulated_mlp(sp, emb[:, :63], emb[:, 63:], mk, gout, fwd_exact=dtype == "bf16x3f")
         got = raw.detach().cpu().double()
+        if dtype == "bf16x3f":
+            np.testing.assert_allclose(got.numpy(), ref_raw.numpy(), rtol=0, atol=1e-4)
         errs["raw"] = float((got - ref_raw).abs().max()) / float(ref_raw.abs().max())
         for name, prm_g in zip(ops.NET_PARAM_NAMES, params):
             r = ref_g[name].reshape(prm_g.shape)
@@ -490,6 +501,38 @@ def test_mlp_backward_kernel_masks(cuda, ops, O, seeded_state, dtype, M):
 
 
 # ---------------------------------------------------------------------------------- grid
+def test_bf16x3f_stores_are_the_bf16x3_hi_halves(cuda, ops, seeded_state):
+    """bf16x3f's training forward (csrc/mlp.hip FwdWave HALF) is the bf16x3 forward with bf16
+    stores: raw and the ReLU masks bit-identical to bf16x3's, and every stored tile-block equal to
+    the hi half (the first two 1 KiB chunks) of bf16x3's 4 KiB tile-block, in the bf16 layout the
+    bf16 dX / dW kernels read."""
+    from nerf_amd._lib import lib, ptr, stream_of
+    g = torch.Generator().manual_seed(21)
+    M, spd = 20010, 10
+    pts = (torch.rand(M, 3, generator=g) * 3 - 1.5).to(cuda)
+    vd = torch.nn.functional.normalize(torch.randn(-(-M // spd), 3, generator=g), dim=-1).to(cuda)
+    params = [seeded_state[f"model.{n}"].to(cuda).clone() for n in ops.NET_PARAM_NAMES]
+    packer = ops.PackedMLP(params)
+    out = {}
+    for code in (ops.BF16X3, ops.BF16X3F):
+        act = torch.zeros(lib().nerf_mlp_act_bytes(code, M), dtype=torch.uint8, device=cuda)
+        masks = torch.zeros(lib().nerf_mlp_mask_bytes(M), dtype=torch.uint8, device=cuda)
+        raw = torch.empty(M, 4, device=cuda)
+        assert lib().nerf_mlp_fwd(ptr(packer.get(code, 0)), code, ptr(pts), ptr(vd), spd, None, M, 1, ptr(raw), ptr(act),
+                                  ptr(masks), stream_of(pts)) == 0
+        out[code] = (raw, act, masks)
+    torch.cuda.synchronize()
+    (r3, a3, m3), (rf, af, mf) = out[ops.BF16X3], out[ops.BF16X3F]
+    assert torch.equal(r3, rf) and torch.equal(m3, mf)
+    nblk = lib().nerf_mlp_padded_samples(M) // 32
+    assert af.numel() * 2 == a3.numel() == nblk * 79 * 4096
+    hi = a3.view(nblk, 79, 4, 1024)[:, :, :2]
+    assert torch.equal(hi.reshape(-1), af)
+    # and the bf16x3f packs are the bf16x3 forward pack and the bf16 backward pack
+    assert torch.equal(packer.get(ops.BF16X3F, 0), packer.get(ops.BF16X3, 0))
+    assert torch.equal(packer.get(ops.BF16X3F, 1), packer.get(ops.BF16, 1))
+
+
 def test_grid_index_bit_exact(golden, cuda, ops):
     pts = torch.from_numpy(golden["grid_pts"]).to(cuda)
     idx, _ = ops.grid_index(pts, None, 128)

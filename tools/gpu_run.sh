@@ -30,10 +30,11 @@ run() {  # run NAME SECONDS CMD...
     exit $r
   fi
 }
+nm=0
 for step in "$@"; do
   case "$step" in
     tests) run tests 1000 $PYT --maxfail=10 tests ;;
-    tests=*) run "tests_k" 900 $PYT --maxfail=10 tests -k "${step#tests=}" ;;
+    tests=*) nm=$((nm + 1)); run "tests_k$nm" 900 $PYT --maxfail=10 tests -k "${step#tests=}" ;;
     file=*) f=${step#file=}; run "file_$(basename $f .py)" 900 $PYT --maxfail=10 "$f" ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) run bench 600 python3 -u bench.py ;;
@@ -44,7 +45,7 @@ for step in "$@"; do
           run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- \
             python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-eager-baseline ;;
     pmc=*) run "pmc_${step#pmc=}" 900 bash tools/gpu_pmc_mlp.sh "${step#pmc=}" ;;
-    mlp=*) args=${step#mlp=}; run mlp 600 python3 tools/mlp_bench.py ${args//+/ } ;;
+    mlp=*) args=${step#mlp=}; nm=$((nm + 1)); run "mlp$nm" 600 python3 tools/mlp_bench.py ${args//+/ } ;;
     march=*) run "march_${step#march=}" 400 python3 tools/march_bench.py --dtype "${step#march=}" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
