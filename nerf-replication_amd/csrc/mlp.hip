@@ -493,6 +493,25 @@ __host__ __device__ constexpr bool finished_in_group(int g, int u) {
   return prev || (u >= G.u0 && (u < last || (u == last && g + 1 == T.n)));
 }
 
+// Scheduling pattern of the group bodies: each MFMA followed by up to IL VALU instructions
+// (sched_group_barrier; 0 = hipcc's own schedule).  A one-wave-per-SIMD kernel (fp32, bf16x3)
+// hides about 5 single-issue instructions per 32-cycle MFMA gap (MI355X_MICROARCH.md).
+#ifndef NERF_IL_VALU_F32
+#define NERF_IL_VALU_F32 0
+#endif
+#ifndef NERF_IL_VALU_BF16
+#define NERF_IL_VALU_BF16 0
+#endif
+#ifndef NERF_IL_VALU_BF3
+#define NERF_IL_VALU_BF3 0
+#endif
+template <class P> __host__ __device__ constexpr int interleave_valu() {
+  return P::KIND == K_F32 ? NERF_IL_VALU_F32 : P::KIND == K_BF16 ? NERF_IL_VALU_BF16 : NERF_IL_VALU_BF3;
+}
+template <class P> __host__ __device__ constexpr int mfma_per_step(int c) {
+  return P::KIND == K_F32 ? 4 : P::KIND == K_BF16 ? 1 : (c < 2 ? 2 : 1);
+}
+
 // W: the wave object; it provides in_tile<u, t>(), prefetch<u>() (issue unit u's side
 // reads one unit ahead), init<u>(acc) (initial accumulator), finish<u>(acc) and a
 // pending accumulator `pend` that carries a finished chain to its deferred finish
@@ -520,11 +539,22 @@ __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
       ring[k % PDP] = as_uint4(wl[N.off * 64]);
     }
     if constexpr (S.first) {
+      // (interleaving: one scheduling region per unit keeps the pipeline solver's work small)
+      if constexpr (interleave_valu<P>() > 0 && S.j > 0) __builtin_amdgcn_sched_barrier(0);
       if constexpr (S.j > 0) w.pend = acc;
       w.template init<S.u>(acc);
       if constexpr (S.j + 1 < G.n) w.template prefetch<S.u + 1>();
     }
     acc = P::mma(a, w.template in_tile<S.u, S.t>(), S.c, acc);
+    if constexpr (interleave_valu<P>() > 0) {
+      // pipeline this step's MFMAs with up to IL VALU each: hipcc otherwise issues a unit's
+      // epilogue (ReLU, mask bits, hi/lo split, stores: ~200 VALU) as one run between two
+      // MFMAs, and with one wave per SIMD nothing else feeds the matrix pipe meanwhile
+      sfor<mfma_per_step<P>(S.c)>([&](auto) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, interleave_valu<P>(), 0);
+      });
+    }
     constexpr int U_BEFORE = S.j > 0 ? S.u - 1 : PREV_U;
     if constexpr (U_BEFORE >= 0 && finished_in_group<DIR, DENSITY, P::CH, cross_finish<P, DIR>()>(g, U_BEFORE) &&
                   S.kin == (FINISH_DELAY < S.len - 1 ? FINISH_DELAY : S.len - 1))

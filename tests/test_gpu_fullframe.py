@@ -1,0 +1,125 @@
+"""BASELINE configs 2 and 4 at full size on the trained net.
+
+Fixture: tests/golden/golden_v4.npz, written by the REFERENCE on the CPU (make_golden_v4.py):
+the trained weights (trained_v2.npz) render the WHOLE 800x800 held-out view of golden_v2 with
+``render()`` (hierarchical, volume_renderer.py:137-247) and with ``render_accelerated()`` (the
+grid march, :268-357) on the reference's own res-128 bake of those weights
+(occupancy_grid.main(), golden_v2).  It keeps every key of 4,096 of the frame's rays (3,072
+uniform + 1,024 over the object's central crop), the float64 row sums of every key, the
+evaluator's uint8 frame and the march's query count over the frame.
+
+Here the whole 640,000-ray frame goes through the drop-in Renderer -- render() in its
+262,144-ray render chunks (M = 50.3 M fine samples per MLP launch), render_accelerated() in one
+march -- and is compared with NO exclusions:
+  * the 4,096 rays, every key: within 1e-4 (fp32); bf16x3 / bf16x3f within 2e-3 on every value
+    and 1e-4 on >= 95 % (the trained-net tolerances of test_gpu_trained.py);
+  * every row sum within 800 x the per-value tolerance (so every row of the frame is covered,
+    not only the sampled rays);
+  * the uint8 frame (clip(rgb) x 255, truncated): every pixel within one level, >= 99.9 %
+    identical (fp32);
+  * the march's MLP query count over the frame.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+os.environ.setdefault("NERF_AMD_NO_ARGV", "1")
+HERE = os.path.dirname(os.path.abspath(__file__))
+H = W = 800
+RENDER_KEYS = ["rgb_map_c", "depth_map_c", "acc_map_c", "rgb_map_f", "depth_map_f", "acc_map_f"]
+MARCH_KEYS = ["rgb_map_f", "depth_map_f", "acc_map_f"]
+TOL = {"fp32": 1e-4, "bf16x3": 1e-4, "bf16x3f": 1e-4}
+MAXERR = {"fp32": 1e-4, "bf16x3": 2e-3, "bf16x3f": 2e-3}
+
+
+@pytest.fixture(scope="module")
+def g4():
+    return np.load(os.path.join(HERE, "golden", "golden_v4.npz"), allow_pickle=False)
+
+
+@pytest.fixture(scope="module")
+def frame(g4, cuda):
+    """The frame's 640,000 rays (oracle get_rays = blender.get_rays, pixel j*W + i); the
+    sampled rays must be the reference's own, bit for bit."""
+    from oracle import nerf_oracle as O
+    o, d = O.get_rays(H, W, float(g4["focal"]), torch.from_numpy(g4["pose"]))
+    rays = torch.cat([o.reshape(-1, 3), d.reshape(-1, 3)], 1)
+    np.testing.assert_array_equal(rays[torch.from_numpy(g4["pix"])].numpy(), g4["rays"])
+    return rays.to(cuda)
+
+
+@pytest.fixture()
+def renderer(cuda):
+    from src.config import cfg
+    from src.models.nerf.network import Network
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    z = np.load(os.path.join(HERE, "golden", "trained_v2.npz"), allow_pickle=False)
+    cfg.task_arg.perturb = 0
+    torch.manual_seed(0)
+    net = Network()
+    net.load_state_dict({k: torch.from_numpy(z[k]) for k in z.files}, strict=True)
+    net = net.to(cuda).eval()
+    yield net, Renderer(net)
+    cfg.task_arg.mlp_dtype = "fp32"
+
+
+def _compare(out, g4, prefix, keys, dtype):
+    pix = torch.from_numpy(g4["pix"]).to(out[keys[0]].device)
+    tol, maxerr = TOL[dtype], MAXERR[dtype]
+    report = {}
+    for k in keys:
+        full = out[k]
+        assert full.shape[0] == H * W, (k, tuple(full.shape))
+        got, ref = full[pix].cpu().numpy(), g4[f"{prefix}_{k}"]
+        err = np.abs(got.astype(np.float64) - ref)
+        frac = float((err <= tol).mean())
+        report[k] = (float(err.max()), frac)
+        assert err.max() <= maxerr and frac >= (1.0 if dtype == "fp32" else 0.95), (prefix, k, dtype, err.max(), frac)
+        rows = full.double().reshape(H, W, -1).sum(1).cpu().numpy()
+        rref = g4[f"{prefix}_rowsum_{k}"].reshape(H, -1)
+        rerr = float(np.abs(rows - rref).max())
+        report[k] += (rerr,)
+        assert rerr <= W * maxerr, (prefix, k, dtype, rerr)
+    print(f"\n{prefix} {dtype}: " + ", ".join(f"{k} max {m:.1e} (<=tol {f:.4f}, row {r:.1e})"
+                                           for k, (m, f, r) in report.items()))
+    img = (out["rgb_map_f"].clamp(0, 1) * 255).to(torch.uint8).reshape(H, W, 3).cpu().numpy()
+    d = np.abs(img.astype(int) - g4[f"{prefix}_frame_u8"].astype(int))
+    print(f"{prefix} {dtype} uint8 frame: max {d.max()}, identical {(d == 0).mean():.5f}")
+    assert d.max() <= (1 if dtype == "fp32" else 2) and (d == 0).mean() >= (0.999 if dtype == "fp32" else 0.99)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16x3f"])
+def test_config2_full_frame_render(g4, frame, renderer, dtype):
+    """Config 2: the 800x800 frame through Renderer.render (262,144-ray render chunks)."""
+    net, r = renderer
+    net.mlp_dtype = dtype
+    near, far = torch.tensor([2.0], device=frame.device), torch.tensor([6.0], device=frame.device)
+    with torch.no_grad():
+        out = r.render({"rays": frame, "near": near, "far": far})
+    _compare(out, g4, "render", RENDER_KEYS, dtype)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3"])
+def test_config4_full_frame_march(g4, frame, renderer, dtype):
+    """Config 4: the frame through render_accelerated on the reference's res-128 bake of the
+    same weights; the MLP query count over all 640,000 rays against the reference's."""
+    net, r = renderer
+    net.mlp_dtype = dtype
+    g2 = np.load(os.path.join(HERE, "golden", "golden_v2.npz"), allow_pickle=False)
+    grid = torch.from_numpy(np.unpackbits(g2["bake128_packed"])[: 128 ** 3].reshape(128, 128, 128).astype(bool))
+    r.set_occupancy_grid(grid, frame.device)
+    np.testing.assert_array_equal(
+        torch.arange(2.0, 6.0, 0.005).numpy(), g4["march_t_table"])  # the t table, as the reference built it
+    near, far = torch.tensor([2.0], device=frame.device), torch.tensor([6.0], device=frame.device)
+    with torch.no_grad():
+        out = r.render_accelerated({"rays": frame, "near": near, "far": far})
+    _compare(out, g4, "march", MARCH_KEYS, dtype)
+    ref_q = int(g4["march_queried"])
+    print(f"march {dtype}: queried {out['n_queried']} (reference {ref_q}), evaluated {out['n_evaluated']}")
+    if dtype == "fp32":
+        assert out["n_queried"] == ref_q
+    else:
+        assert abs(out["n_queried"] - ref_q) <= 1e-4 * ref_q

@@ -7,9 +7,8 @@ depend on the batch:
   alone (sampling, importance sampling + merge, compositing, and the whole bf16 render);
 - structure: stratified and merged depths sorted and inside [near, far], the merged depths contain
   the coarse depths, points = o + d*z as the reference rounds them, weights >= 0, acc in [0, 1];
-- a sampled subset of the full frame against the oracle, at the bf16 tolerance of
-  test_gpu_render.test_render_perturb0 (north_star: rgb/depth 2e-3, depth scaled by its range 6),
-  leaving out the few rays on the reference's last-sample discontinuity (see the test).
+- parity with the reference at full size lives in test_gpu_fullframe.py (the trained net's whole
+  800x800 frame against reference-rendered goldens, no exclusions).
 Empty (R = 0) and ragged (R not a multiple of the wave / block size) batches are covered too.
 """
 import os
@@ -110,10 +109,13 @@ def test_empty_batches(cuda, ops):
     assert out["z_fine"].shape == (0, 192) and out["pts_fine"].shape == (0, 192, 3)
 
 
-def test_full_frame_render_row_independent_and_matches_oracle(cuda, ops, O, seeded_state, frame_rays):
+def test_full_frame_render_row_independent(cuda, ops, seeded_state, frame_rays):
     """One 800x800 view (640,000 rays, 262,144-ray render chunks) through the drop-in Renderer with
-    the bf16 MLP: a ragged subset rendered alone is bit-identical to the same rays in the frame,
-    and 48 rays of the frame agree with the oracle (fp32 reference restatement)."""
+    the bf16 MLP on the untrained seed-0 net: finite outputs, acc in [0, 1], and a ragged subset
+    rendered alone bit-identical to the same rays in the frame.  Parity with the reference at
+    this size is pinned on the trained net, every ray of 4,096 and every row of the frame, with no
+    exclusions (test_gpu_fullframe.py, golden_v4); the seed-0 net's oracle comparison, which had
+    to leave out rays whose last-sample density changes sign, is retired."""
     from src.config import cfg
     from src.models.nerf.network import Network
     from src.models.nerf.renderer.volume_renderer import Renderer
@@ -121,59 +123,22 @@ def test_full_frame_render_row_independent_and_matches_oracle(cuda, ops, O, seed
     cfg.task_arg.mlp_dtype = "bf16"
     cfg.task_arg.perturb = 0
     try:
-        _render_checks(cfg, cuda, O, seeded_state, frame_rays, Network, Renderer)
+        torch.manual_seed(0)
+        net = Network().to(cuda)
+        net.mlp_dtype = "bf16"
+        net.eval()
+        r = Renderer(net)
+        near, far = torch.tensor([2.0], device=cuda), torch.tensor([6.0], device=cuda)
+        keys = ["rgb_map_c", "depth_map_c", "acc_map_c", "rgb_map_f", "depth_map_f", "acc_map_f"]
+        with torch.no_grad():
+            full = r.render({"rays": frame_rays[None], "near": near, "far": far})
+            for k in keys:
+                assert full[k].shape[0] == H * W, k
+                assert torch.isfinite(full[k]).all(), k
+            assert float(full["acc_map_f"].min()) >= 0.0 and float(full["acc_map_f"].max()) <= 1.0 + 1e-5
+            idx = _subset(1001, H * W, 2).to(cuda)
+            part = r.render({"rays": frame_rays[idx][None], "near": near, "far": far})
+        for k in keys:
+            assert torch.equal(part[k], full[k][idx]), k
     finally:
         cfg.task_arg.mlp_dtype, cfg.task_arg.perturb = saved
-
-
-def _render_checks(cfg, cuda, O, seeded_state, frame_rays, Network, Renderer):
-    torch.manual_seed(0)
-    net = Network().to(cuda)
-    net.mlp_dtype = "bf16"
-    net.eval()
-    r = Renderer(net)
-    near, far = torch.tensor([2.0], device=cuda), torch.tensor([6.0], device=cuda)
-    keys = ["rgb_map_c", "depth_map_c", "acc_map_c", "rgb_map_f", "depth_map_f", "acc_map_f"]
-    with torch.no_grad():
-        full = r.render({"rays": frame_rays[None], "near": near, "far": far})
-        for k in keys:
-            assert full[k].shape[0] == H * W, k
-            assert torch.isfinite(full[k]).all(), k
-        assert float(full["acc_map_f"].min()) >= 0.0 and float(full["acc_map_f"].max()) <= 1.0 + 1e-5
-        idx = _subset(1001, H * W, 2).to(cuda)
-        part = r.render({"rays": frame_rays[idx][None], "near": near, "far": far})
-    for k in keys:
-        assert torch.equal(part[k], full[k][idx]), k
-
-    C, Fn = O.split_params(seeded_state, "model"), O.split_params(seeded_state, "model_fine")
-    sub = _subset(96, H * W, 3)
-    with torch.no_grad():
-        ref = O.render(C, Fn, frame_rays[sub.to(cuda)].cpu(), torch.tensor([2.0]), torch.tensor([6.0]), keep=True)
-    # The reference's last interval is 1e10 long (volume_renderer.py:42): the last sample's alpha
-    # jumps from 0 to 1 as sigma = ReLU(raw[3]) leaves 0, so a ray whose last pre-activation
-    # changes sign between the fp32 reference and the bf16 MLP takes the last sample's colour
-    # instead of the white background.  That is a discontinuity of the reference, not a
-    # tolerance question.  Such rays are found exactly, from this MLP's own raw at the last sample
-    # (z = far for both passes, since the merge keeps the coarse depths), counted, and left out
-    # of the tolerance check.  The coarse weights passed to sample_pdf exclude the last sample
-    # (volume_renderer.py:214), so a coarse flip does not reach the fine pass.
-    rs = frame_rays[sub.to(cuda)]
-    last = (rs[:, :3] + rs[:, 3:] * 6.0)[:, None, :]
-    vd = rs[:, 3:] / torch.norm(rs[:, 3:], dim=-1, keepdim=True)
-    with torch.no_grad():
-        ours = {"c": net(last, vd, "")[:, 0, 3].cpu(), "f": net(last, vd, "fine")[:, 0, 3].cpu()}
-    unstable = {p: (ours[p] > 0) != (ref[f"raw_{p}"][:, -1, 3] > 0) for p in "cf"}
-    assert int(unstable["c"].sum()) + int(unstable["f"].sum()) <= len(sub) // 8, unstable
-    for k in keys:
-        keep = ~unstable[k[-1]]
-        tol = 2e-3 * (6.0 if "depth" in k else 1.0)
-        got, want = full[k][sub.to(cuda)].cpu()[keep].numpy(), ref[k][keep].numpy()
-        if k.endswith("_f"):
-            # end to end the fine pass sees the CDF of bf16 coarse weights, so a few importance
-            # samples move to a neighbouring bin (see test_gpu_render.E2E_FINE_DEPTH_TOL for the
-            # fp32 case); given the same samples the fine pass is held to the plain tolerance
-            # (test_gpu_render.test_fine_pass_given_reference_samples).  Here: 95 % of the rays
-            # within the plain tolerance, all within twice it.
-            assert np.mean(np.abs(got - want) <= tol) >= 0.95, (k, np.abs(got - want).max())
-            tol *= 2
-        np.testing.assert_allclose(got, want, rtol=0, atol=tol, err_msg=f"{k}: rays {sub[keep].tolist()}")

@@ -17,7 +17,7 @@
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-PYT="python -u -m pytest -m gpu -v --timeout 300 --timeout-method thread"
+PYT="python -u -m pytest -m gpu -v -s --timeout 300 --timeout-method thread"
 run() {  # run NAME SECONDS CMD...
   local name=$1 secs=$2; shift 2
   echo "[gpu_run] $name: $*"
