@@ -122,6 +122,9 @@ int nerf_mlp_bwd(const void* packed_bwd, int dtype, const float* d_raw, int64_t 
 /* the two halves of nerf_mlp_bwd (dX chain kernel, dW/db GEMM kernel) as separate calls */
 int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64_t M, const uint16_t* masks, void* dz,
                     hipStream_t stream);
+/* nerf_mlp_bwd_dw (= the _ws form with workspace NULL) adds the work items' partial sums with fp32
+ * atomics: NOT bit-reproducible run to run (the sum order varies).  The production path (ops.py,
+ * DETERMINISTIC_DW) uses nerf_mlp_bwd_dw_ws with a workspace. */
 int nerf_mlp_bwd_dw(int dtype, int64_t M, const void* act, const void* dz, float* grad, hipStream_t stream);
 /* dW/db with a workspace of nerf_mlp_dw_workspace_bytes(dtype, M): each work item writes its partial
  * sums to its own slice and a second kernel adds them per parameter in a fixed order, so the gradient

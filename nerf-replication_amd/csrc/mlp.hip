@@ -82,6 +82,11 @@ struct PF32 {
     return make_uint4(__float_as_uint(t.v[4 * c]), __float_as_uint(t.v[4 * c + 1]), __float_as_uint(t.v[4 * c + 2]),
                       __float_as_uint(t.v[4 * c + 3]));
   }
+  // registers 2k, 2k + 1 of a tile (the finish writes a tile pair by pair)
+  static __device__ __forceinline__ void set_pair(Tile& t, int k, float x0, float x1) {
+    t.v[2 * k] = x0;
+    t.v[2 * k + 1] = x1;
+  }
 };
 
 struct PBF16 {
@@ -121,6 +126,18 @@ struct PBF16 {
     return s;
   }
   static __device__ __forceinline__ uint4 chunk(const Tile& t, int c) { return __builtin_bit_cast(uint4, t.b[c]); }
+  // packed pair k (registers 2k, 2k + 1) = dword k & 3 of chunk k >> 2
+  static __device__ __forceinline__ void set_dword(Tile& t, int k, uint32_t d) {
+    uint4 v = __builtin_bit_cast(uint4, t.b[k >> 2]);
+    if ((k & 3) == 0) v.x = d;
+    else if ((k & 3) == 1) v.y = d;
+    else if ((k & 3) == 2) v.z = d;
+    else v.w = d;
+    t.b[k >> 2] = __builtin_bit_cast(bf16x8, v);
+  }
+  static __device__ __forceinline__ void set_pair(Tile& t, int k, float x0, float x1) {
+    set_dword(t, k, pack_bf16(x0, x1));
+  }
 };
 
 // bf16x3: every fp32 operand x is split x = hi + lo (hi = bf16(x), lo = bf16(x - hi), 16
@@ -176,6 +193,21 @@ struct PBF3 {
   }
   static __device__ __forceinline__ uint4 chunk(const Tile& t, int c) {
     return __builtin_bit_cast(uint4, c < 2 ? t.hi[c] : t.lo[c - 2]);
+  }
+  static __device__ __forceinline__ void put(bf16x8& dst, int q, uint32_t d) {
+    uint4 v = __builtin_bit_cast(uint4, dst);
+    if (q == 0) v.x = d;
+    else if (q == 1) v.y = d;
+    else if (q == 2) v.z = d;
+    else v.w = d;
+    dst = __builtin_bit_cast(bf16x8, v);
+  }
+  // registers 2k, 2k + 1 split into hi / lo pairs (the values pack16 gives)
+  static __device__ __forceinline__ void set_pair(Tile& t, int k, float x0, float x1) {
+    const uint32_t hw = pack_bf16(x0, x1);
+    const uint32_t lw = pack_bf16(x0 - __uint_as_float(hw << 16), x1 - __uint_as_float(hw & 0xffff0000u));
+    put(t.hi[k >> 2], k & 3, hw);
+    put(t.lo[k >> 2], k & 3, lw);
   }
 };
 
@@ -466,7 +498,7 @@ template <class P> __host__ __device__ constexpr int prefetch_depth() {
 constexpr int FINISH_DELAY = NERF_FINISH_DELAY;
 
 // W: the wave object; it provides in_tile<u, t>(), prefetch<u>() (issue unit u's side
-// reads one unit ahead), init<u>(acc) (initial accumulator) and finish<u>(acc)
+// reads one unit ahead), init<u>(acc) (initial accumulator) and finish_part<u, p>(acc)
 #ifndef NERF_CROSS_GROUP_FINISH
 #define NERF_CROSS_GROUP_FINISH 1
 #endif
@@ -493,35 +525,94 @@ __host__ __device__ constexpr bool finished_in_group(int g, int u) {
   return prev || (u >= G.u0 && (u < last || (u == last && g + 1 == T.n)));
 }
 
-// Scheduling pattern of the group bodies: each MFMA followed by up to IL VALU instructions
-// (sched_group_barrier; 0 = hipcc's own schedule).  A one-wave-per-SIMD kernel (fp32, bf16x3)
-// hides about 5 single-issue instructions per 32-cycle MFMA gap (MI355X_MICROARCH.md).
-#ifndef NERF_IL_VALU_F32
-#define NERF_IL_VALU_F32 0
+// Finish parts.  A unit's epilogue (ReLU, mask bits, pack / hi-lo split, stores: ~60-110
+// instructions) issued as one run stalls the matrix pipe of a one-wave-per-SIMD kernel (fp32,
+// bf16x3) for the whole run: nothing else feeds it (the gfx950 assembly of the bf16x3
+// training forward had 70 % of its non-MFMA instructions in 138 runs of > 20 between two
+// MFMAs).  With NP parts, part p (register pairs [8p/NP, 8(p+1)/NP)) is issued FINISH_DELAY + p
+// steps into the next unit, clamped to that unit's last step; the last part stores.
+#ifndef NERF_FINISH_PARTS_F32
+#define NERF_FINISH_PARTS_F32 1
 #endif
-#ifndef NERF_IL_VALU_BF16
-#define NERF_IL_VALU_BF16 0
+#ifndef NERF_FINISH_PARTS_BF16
+#define NERF_FINISH_PARTS_BF16 1
 #endif
-#ifndef NERF_IL_VALU_BF3
-#define NERF_IL_VALU_BF3 0
+#ifndef NERF_FINISH_PARTS_BF3
+#define NERF_FINISH_PARTS_BF3 1
 #endif
-template <class P> __host__ __device__ constexpr int interleave_valu() {
-  return P::KIND == K_F32 ? NERF_IL_VALU_F32 : P::KIND == K_BF16 ? NERF_IL_VALU_BF16 : NERF_IL_VALU_BF3;
+template <class P> __host__ __device__ constexpr int finish_parts() {
+  return P::KIND == K_F32 ? NERF_FINISH_PARTS_F32 : P::KIND == K_BF16 ? NERF_FINISH_PARTS_BF16 : NERF_FINISH_PARTS_BF3;
 }
-template <class P> __host__ __device__ constexpr int mfma_per_step(int c) {
-  return P::KIND == K_F32 ? 4 : P::KIND == K_BF16 ? 1 : (c < 2 ? 2 : 1);
+// DMA spread.  0: the next group's LDS-DMA pieces (up to 18 per wave, ~7 instructions each)
+// are issued as one burst at the group's start; S > 0: piece i at step i (NS / S) / NF of the
+// group's NS steps, i.e. inside the first 1/S of the group (they must land before its end).
+#ifndef NERF_DMA_SPREAD_F32
+#define NERF_DMA_SPREAD_F32 0
+#endif
+#ifndef NERF_DMA_SPREAD_BF16
+#define NERF_DMA_SPREAD_BF16 0
+#endif
+#ifndef NERF_DMA_SPREAD_BF3
+#define NERF_DMA_SPREAD_BF3 0
+#endif
+template <class P> __host__ __device__ constexpr int dma_spread() {
+  return PF != 1 ? 0 : P::KIND == K_F32 ? NERF_DMA_SPREAD_F32 : P::KIND == K_BF16 ? NERF_DMA_SPREAD_BF16 : NERF_DMA_SPREAD_BF3;
+}
+
+// step (in group g) at which part p of unit u's finish is issued, or -1 when u is not
+// finished in g
+template <class P, int DIR, bool DENSITY>
+__host__ __device__ constexpr int part_step(int g, int u, int p) {
+  const auto& T = GroupTable<DIR, DENSITY, P::CH>::t;
+  const Group G = T.g[g];
+  if (!finished_in_group<DIR, DENSITY, P::CH, cross_finish<P, DIR>()>(g, u)) return -1;
+  const int NS = group_steps<DIR, DENSITY, P::CH>(g);
+  if (u == G.u0 + G.n - 1) return NS - 1;  // the group's last unit, finished in-group: at its last step
+  const int js = u < G.u0 ? 0 : u - G.u0 + 1;  // the unit after u (this group's first, or u + 1)
+  int start = 0;
+  for (int j = 0; j < js; ++j) start += unit_tiles<DIR>(G.u0 + j) * P::CH;
+  const int len = unit_tiles<DIR>(G.u0 + js) * P::CH;
+  const int d = FINISH_DELAY + p;
+  return start + (d < len - 1 ? d : len - 1);
+}
+// step (in group g) of the i-th of the next group's NF DMA pieces (dma_spread > 0)
+template <class P, int DIR, bool DENSITY>
+__host__ __device__ constexpr int dma_piece_step(int g, int i) {
+  const int NS = group_steps<DIR, DENSITY, P::CH>(g);
+  const int NF = group_dma<P, DIR, DENSITY>(g + 1);
+  const int front = (NS + dma_spread<P>() - 1) / dma_spread<P>();
+  return i * front / NF;
+}
+// vmcnt of the hand-off at the end of group g when the next group's DMA is spread over
+// group g: the stores issued at or after the step of its last piece (a step issues its DMA
+// pieces first, then its MFMAs, then any finish parts)
+template <class P, int DIR, bool DENSITY, class StoresFn>
+__host__ __device__ constexpr int handoff_vmcnt_spread(int g, StoresFn unit_stores) {
+  if (g + 1 >= GroupTable<DIR, DENSITY, P::CH>::t.n) return 0;  // (the last group: no hand-off)
+  const int last = dma_piece_step<P, DIR, DENSITY>(g, group_dma<P, DIR, DENSITY>(g + 1) - 1);
+  const int NU = DIR == 0 ? NUNIT_FWD : NUNIT_BWD;
+  int n = 0;
+  for (int u = 0; u < NU; ++u) {
+    const int s = part_step<P, DIR, DENSITY>(g, u, finish_parts<P>() - 1);
+    if (s >= last) n += unit_stores(u);
+  }
+  return n;
 }
 
 // W: the wave object; it provides in_tile<u, t>(), prefetch<u>() (issue unit u's side
-// reads one unit ahead), init<u>(acc) (initial accumulator), finish<u>(acc) and a
-// pending accumulator `pend` that carries a finished chain to its deferred finish
+// reads one unit ahead), init<u>(acc) (initial accumulator), finish_part<u, p>(acc),
+// fetch_piece<g, i>() (the i-th DMA piece of group g) and a pending accumulator `pend` that
+// carries a finished chain to its deferred finish
 template <class P, int DIR, bool DENSITY, int g, class W>
 __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
   constexpr int NS = group_steps<DIR, DENSITY, P::CH>(g);
   constexpr int PDP = prefetch_depth<P>();
+  constexpr int NP = finish_parts<P>();
   constexpr auto& T = GroupTable<DIR, DENSITY, P::CH>::t;
   constexpr Group G = T.g[g];
   constexpr int PREV_U = g > 0 ? T.g[g - 1].u0 + T.g[g - 1].n - 1 : -1;  // previous group's last unit
+  constexpr bool SPREAD = dma_spread<P>() > 0 && g + 1 < T.n;
+  constexpr int NF = SPREAD ? group_dma<P, DIR, DENSITY>(g + 1) : 0;
   uint4 ring[PDP];
   sfor<(NS < PDP ? NS : PDP)>([&](auto kk) {
     constexpr int k = decltype(kk)::value;
@@ -533,34 +624,33 @@ __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
   sfor<NS>([&](auto kk) {
     constexpr int k = decltype(kk)::value;
     constexpr Step S = group_step<DIR, DENSITY, P::CH>(g, k);
+    if constexpr (SPREAD) {
+      sfor<NF>([&](auto ii) {
+        if constexpr (dma_piece_step<P, DIR, DENSITY>(g, decltype(ii)::value) == k)
+          w.template fetch_piece<g + 1, decltype(ii)::value>();
+      });
+    }
     const uint4 a = ring[k % PDP];
     if constexpr (k + PDP < NS) {
       constexpr Step N = group_step<DIR, DENSITY, P::CH>(g, k + PDP);
       ring[k % PDP] = as_uint4(wl[N.off * 64]);
     }
     if constexpr (S.first) {
-      // (interleaving: one scheduling region per unit keeps the pipeline solver's work small)
-      if constexpr (interleave_valu<P>() > 0 && S.j > 0) __builtin_amdgcn_sched_barrier(0);
       if constexpr (S.j > 0) w.pend = acc;
       w.template init<S.u>(acc);
       if constexpr (S.j + 1 < G.n) w.template prefetch<S.u + 1>();
     }
     acc = P::mma(a, w.template in_tile<S.u, S.t>(), S.c, acc);
-    if constexpr (interleave_valu<P>() > 0) {
-      // pipeline this step's MFMAs with up to IL VALU each: hipcc otherwise issues a unit's
-      // epilogue (ReLU, mask bits, hi/lo split, stores: ~200 VALU) as one run between two
-      // MFMAs, and with one wave per SIMD nothing else feeds the matrix pipe meanwhile
-      sfor<mfma_per_step<P>(S.c)>([&](auto) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, interleave_valu<P>(), 0);
+    constexpr int U_BEFORE = S.j > 0 ? S.u - 1 : PREV_U;
+    if constexpr (U_BEFORE >= 0) {
+      sfor<NP>([&](auto pp) {
+        if constexpr (part_step<P, DIR, DENSITY>(g, U_BEFORE, decltype(pp)::value) == k)
+          w.template finish_part<U_BEFORE, decltype(pp)::value>(w.pend);
       });
     }
-    constexpr int U_BEFORE = S.j > 0 ? S.u - 1 : PREV_U;
-    if constexpr (U_BEFORE >= 0 && finished_in_group<DIR, DENSITY, P::CH, cross_finish<P, DIR>()>(g, U_BEFORE) &&
-                  S.kin == (FINISH_DELAY < S.len - 1 ? FINISH_DELAY : S.len - 1))
-      w.template finish<U_BEFORE>(w.pend);
     if constexpr (S.last && S.j == G.n - 1) {
-      if constexpr (finished_in_group<DIR, DENSITY, P::CH, cross_finish<P, DIR>()>(g, S.u)) w.template finish<S.u>(acc);
+      if constexpr (finished_in_group<DIR, DENSITY, P::CH, cross_finish<P, DIR>()>(g, S.u))
+        sfor<NP>([&](auto pp) { w.template finish_part<S.u, decltype(pp)::value>(acc); });
       else w.pend = acc;
     }
   });
@@ -582,6 +672,17 @@ __device__ __forceinline__ void fetch_group(const uint4* gsrc, uint32_t slot_bas
     const int k = cmin(wave + P::WAVES * i, NCH - 1);
     glds16_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
   }
+}
+// the i-th of fetch_group's NF wave-instructions alone (the DMA spread over a group body)
+template <class P, int C0, int NCH, int I, bool LAUNDER = false>
+__device__ __forceinline__ void fetch_piece(const uint4* gsrc, uint32_t slot_base, int wave, int lane) {
+  if constexpr (LAUNDER) {
+    uint32_t w = wave;
+    settle(w);
+    wave = (int)w;
+  }
+  const int k = cmin(wave + P::WAVES * I, NCH - 1);
+  glds16_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
 }
 
 
@@ -796,6 +897,11 @@ struct FwdWave {
     constexpr Group G = GT::t.g[g];
     fetch_group<P, G.c0, G.nch, PERSIST>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
   }
+  template <int g, int i> __device__ __forceinline__ void fetch_piece() {
+    constexpr Group G = GT::t.g[g];
+    nerf::mlp::fetch_piece<P, G.c0, G.nch, i, PERSIST>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024),
+                                                       wave, lane);
+  }
 
   // input tile t of layer L (mlp_tables.h: Ha/Hb ping-pong, PE tiles X / D)
   template <int L, int t> __device__ __forceinline__ const Tile& in_tile_L() const {
@@ -826,75 +932,57 @@ struct FwdWave {
     return s;
   }
 
-  template <int L, int n> __device__ __forceinline__ void finish_L(const f32x16& acc) {
+  // part p of NP of unit (L, n)'s finish: register pairs [8p/NP, 8(p+1)/NP) into the output
+  // tile (in place), their mask bits; the last part stores the tile (and the layer's masks)
+  template <int L, int n, int p> __device__ __forceinline__ void finish_L_part(const f32x16& acc) {
+    constexpr int NP = finish_parts<P>();
+    constexpr int K0 = 8 * p / NP, K1 = 8 * (p + 1) / NP;
+    constexpr bool LASTP = p == NP - 1;
     if constexpr (L <= L7 || L == LV) {
-      Tile out;
-      uint32_t bits = 0;  // mask bits of this tile (mask_bit layout)
-      if constexpr (P::KIND == K_BF16) {
-        // bf16: pack pairs first, then ReLU and mask on the packed pairs (2 values per VALU)
-        uint32_t d[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-#if NERF_MASK_FROM_PACKED
-          d[k] = relu_bf16x2(pack_bf16(acc[2 * k], acc[2 * k + 1]));
-          if constexpr (STORE) bits |= nonzero_bf16x2(d[k]) << k;
-#else
+      Tile& out = out_arr<L>()[n];
+      uint32_t bits = 0;  // this tile's mask bits (mask_bit layout)
+      sfor<K1 - K0>([&](auto kk) {
+        constexpr int k = K0 + decltype(kk)::value;
+        const float a0 = acc[2 * k], a1 = acc[2 * k + 1];
+        if constexpr (P::KIND == K_BF16) {
+          // bf16: pack the pair first, then ReLU on the packed pair (one VALU for both)
           if constexpr (STORE) {
-            bits |= (acc[2 * k] > 0.f ? 1u : 0u) << mask_bit(2 * k);
-            bits |= (acc[2 * k + 1] > 0.f ? 1u : 0u) << mask_bit(2 * k + 1);
+            bits |= (a0 > 0.f ? 1u : 0u) << mask_bit(2 * k);
+            bits |= (a1 > 0.f ? 1u : 0u) << mask_bit(2 * k + 1);
           }
-          d[k] = relu_bf16x2(pack_bf16(acc[2 * k], acc[2 * k + 1]));
-#endif
-        }
-        out.b[0] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
-        out.b[1] = __builtin_bit_cast(bf16x8, make_uint4(d[4], d[5], d[6], d[7]));
-      } else {
-        float v[16];
-#pragma unroll
-        for (int rho = 0; rho < 16; ++rho) {
+          P::set_dword(out, k, relu_bf16x2(pack_bf16(a0, a1)));
+        } else {
           // ReLU as an integer max on the float bits (negative floats are negative ints)
-          const int y = max(__float_as_int(acc[rho]), 0);
-          if constexpr (STORE) bits |= (y > 0 ? 1u : 0u) << mask_bit(rho);
-          if constexpr (P::KIND == K_BF16X3) v[rho] = __int_as_float(y);
-          else P::set(out, rho, __int_as_float(y));
+          const int y0 = max(__float_as_int(a0), 0), y1 = max(__float_as_int(a1), 0);
+          if constexpr (STORE) {
+            bits |= min((uint32_t)y0, 1u) << mask_bit(2 * k);
+            bits |= min((uint32_t)y1, 1u) << mask_bit(2 * k + 1);
+          }
+          P::set_pair(out, k, __int_as_float(y0), __int_as_float(y1));
         }
-        if constexpr (P::KIND == K_BF16X3) P::pack16(out, v);
-      }
-      out_arr<L>()[n] = out;
+      });
       if constexpr (STORE) {
-        store_tile<P, SCH>(a.act, a.nblk, AT_TILES, (L == LV ? AT_V : AT_H + 8 * L) + n, wblock, lane, out);
-        if constexpr ((n & 1) == 0) mw[n >> 1] = bits;
-        else mw[n >> 1] |= bits << 8;
-        if constexpr (n == fwd_out_tiles(L) - 1)
-          store16<0>(mask_slot(a.masks, wblock, L == LV ? 8 : L, lane),
-                     make_uint4(mw[0], mw[1], L == LV ? 0u : mw[2], L == LV ? 0u : mw[3]));
+        if constexpr (K0 == 0 && (n & 1) == 0) mw[n >> 1] = bits;
+        else mw[n >> 1] |= bits << (8 * (n & 1));
+        if constexpr (LASTP) {
+          store_tile<P, SCH>(a.act, a.nblk, AT_TILES, (L == LV ? AT_V : AT_H + 8 * L) + n, wblock, lane, out);
+          if constexpr (n == fwd_out_tiles(L) - 1)
+            store16<0>(mask_slot(a.masks, wblock, L == LV ? 8 : L, lane),
+                       make_uint4(mw[0], mw[1], L == LV ? 0u : mw[2], L == LV ? 0u : mw[3]));
+        }
       }
     } else if constexpr (L == LFA) {
       if constexpr (n < 8) {  // feature_linear: no activation
-        Tile out;
-        if constexpr (P::KIND == K_BF16) {
-          uint32_t d[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) d[k] = pack_bf16(acc[2 * k], acc[2 * k + 1]);
-          out.b[0] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
-          out.b[1] = __builtin_bit_cast(bf16x8, make_uint4(d[4], d[5], d[6], d[7]));
-        } else {
-          if constexpr (P::KIND == K_BF16X3) {
-            float v[16];
-#pragma unroll
-            for (int rho = 0; rho < 16; ++rho) v[rho] = acc[rho];
-            P::pack16(out, v);
-          } else {
-#pragma unroll
-            for (int rho = 0; rho < 16; ++rho) P::set(out, rho, acc[rho]);
-          }
-        }
-        Ha[n] = out;
-        if constexpr (STORE) store_tile<P, SCH>(a.act, a.nblk, AT_TILES, AT_F + n, wblock, lane, out);
-      } else {
+        Tile& out = Ha[n];
+        sfor<K1 - K0>([&](auto kk) {
+          constexpr int k = K0 + decltype(kk)::value;
+          P::set_pair(out, k, acc[2 * k], acc[2 * k + 1]);
+        });
+        if constexpr (STORE && LASTP) store_tile<P, SCH>(a.act, a.nblk, AT_TILES, AT_F + n, wblock, lane, out);
+      } else if constexpr (p == 0) {
         alpha = acc[0];  // alpha_linear: output row 0 = register 0 of lanes 0..31
       }
-    } else {  // LRGB: rows 0..2 = registers 0..2 of lanes 0..31
+    } else if constexpr (p == 0) {  // LRGB: rows 0..2 = registers 0..2 of lanes 0..31
       rgb0 = acc[0];
       rgb1 = acc[1];
       rgb2 = acc[2];
@@ -941,19 +1029,20 @@ struct FwdWave {
       acc[4 * q + 3] = __uint_as_float(bias[q].w);
     }
   }
-  template <int u> __device__ __forceinline__ void finish(const f32x16& acc) {
+  template <int u, int p> __device__ __forceinline__ void finish_part(const f32x16& acc) {
     constexpr int L = fwd_unit_layer(u), n = u - fwd_unit_first(L);
-    finish_L<L, n>(acc);
+    finish_L_part<L, n, p>(acc);
   }
 
   template <int g> __device__ __forceinline__ void step() {
     constexpr int NG = GT::t.n;
-    if constexpr (g + PF < NG) fetch<g + PF>();
+    if constexpr (g + PF < NG && dma_spread<P>() == 0) fetch<g + PF>();
     const uint32_t slot = lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024);
     wb = lds_ptr(slot + (uint32_t)(h * 16));
     group_body<P, 0, DENSITY, g>(*this, lds_ptr(slot + (uint32_t)(lane * 16)));
-    constexpr int N = handoff_vmcnt<P, 0, DENSITY>(g, [](int i) constexpr { return group_stores(i); },
-                                                   STORE ? 3 * SCH : 0);
+    constexpr int N = dma_spread<P>() > 0
+        ? handoff_vmcnt_spread<P, 0, DENSITY>(g, [](int u) constexpr { return unit_stores(u); })
+        : handoff_vmcnt<P, 0, DENSITY>(g, [](int i) constexpr { return group_stores(i); }, STORE ? 3 * SCH : 0);
     if constexpr (g + 1 < NG) wait_barrier<N>();
   }
 
@@ -1077,6 +1166,11 @@ struct DxWave {
     constexpr Group Gr = GT::t.g[g];
     fetch_group<P, Gr.c0, Gr.nch>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
   }
+  template <int g, int i> __device__ __forceinline__ void fetch_piece() {
+    constexpr Group Gr = GT::t.g[g];
+    nerf::mlp::fetch_piece<P, Gr.c0, Gr.nch, i>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
+  }
+  static __host__ __device__ constexpr int unit_stores(int) { return CH; }
 
   template <int s, int t> __device__ __forceinline__ const Tile& in_tile_S() const {
     if constexpr (s == B_RGB) return G;
@@ -1112,46 +1206,43 @@ struct DxWave {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   }
-  template <int u> __device__ __forceinline__ void finish(const f32x16& acc) {
+  // part p of NP of unit u's finish: register pairs [8p/NP, 8(p+1)/NP) masked by the forward's
+  // ReLU bits into the output-gradient tile (in place); the last part stores the tile
+  template <int u, int p> __device__ __forceinline__ void finish_part(const f32x16& acc) {
     constexpr int s = bwd_unit_stage(u), j = u - bwd_unit_first(s);
     constexpr int mg = mask_group(s);
+    constexpr int NP = finish_parts<P>();
+    constexpr int K0 = 8 * p / NP, K1 = 8 * (p + 1) / NP;
     uint32_t w = 0xFFFFFFFFu;  // this tile's bits at mask_bit(rho)
     if constexpr (mg >= 0) {
       w = (j >> 1) == 0 ? mk[mg].x : (j >> 1) == 1 ? mk[mg].y : (j >> 1) == 2 ? mk[mg].z : mk[mg].w;
       w >>= 8 * (j & 1);
     }
-    Tile out;
-    if constexpr (P::KIND == K_BF16) {
-      uint32_t d[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        d[k] = pack_bf16(acc[2 * k], acc[2 * k + 1]);
+    Tile& out = out_arr<s>()[j];
+    sfor<K1 - K0>([&](auto kk) {
+      constexpr int k = K0 + decltype(kk)::value;
+      if constexpr (P::KIND == K_BF16) {
+        uint32_t d = pack_bf16(acc[2 * k], acc[2 * k + 1]);
         // bits k, 16 + k -> 0x0000FFFF / 0xFFFF0000 halves (one v_mul_u32_u24)
-        if constexpr (mg >= 0) d[k] &= ((w >> k) & 0x10001u) * 0xFFFFu;
+        if constexpr (mg >= 0) d &= ((w >> k) & 0x10001u) * 0xFFFFu;
+        P::set_dword(out, k, d);
+      } else {
+        const float y0 = ((w >> mask_bit(2 * k)) & 1u) ? acc[2 * k] : 0.f;
+        const float y1 = ((w >> mask_bit(2 * k + 1)) & 1u) ? acc[2 * k + 1] : 0.f;
+        P::set_pair(out, k, y0, y1);
       }
-      out.b[0] = __builtin_bit_cast(bf16x8, make_uint4(d[0], d[1], d[2], d[3]));
-      out.b[1] = __builtin_bit_cast(bf16x8, make_uint4(d[4], d[5], d[6], d[7]));
-    } else {
-      float v[16];
-#pragma unroll
-      for (int rho = 0; rho < 16; ++rho) {
-        const float y = ((w >> mask_bit(rho)) & 1u) ? acc[rho] : 0.f;
-        if constexpr (P::KIND == K_BF16X3) v[rho] = y;
-        else P::set(out, rho, y);
-      }
-      if constexpr (P::KIND == K_BF16X3) P::pack16(out, v);
-    }
-    out_arr<s>()[j] = out;
-    constexpr int dzt = dz_tile(s, j);
-    store_tile<P>(a.dz, a.nblk, ZT_TILES, dzt, wblock, lane, out);
+    });
+    if constexpr (p == NP - 1) store_tile<P>(a.dz, a.nblk, ZT_TILES, dz_tile(s, j), wblock, lane, out);
   }
 
   template <int g> __device__ __forceinline__ void step() {
     constexpr int NG = GT::t.n;
-    if constexpr (g + PF < NG) fetch<g + PF>();
+    if constexpr (g + PF < NG && dma_spread<P>() == 0) fetch<g + PF>();
     const uint32_t slot = lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024);
     group_body<P, 1, false, g>(*this, lds_ptr(slot + (uint32_t)(lane * 16)));
-    constexpr int N = handoff_vmcnt<P, 1, false>(g, [](int i) constexpr { return group_stores(i); }, 2 * CH);
+    constexpr int N = dma_spread<P>() > 0
+        ? handoff_vmcnt_spread<P, 1, false>(g, [](int u) constexpr { return unit_stores(u); })
+        : handoff_vmcnt<P, 1, false>(g, [](int i) constexpr { return group_stores(i); }, 2 * CH);
     if constexpr (g + 1 < NG) wait_barrier<N>();
   }
 

@@ -5,8 +5,9 @@ Same class, methods and output keys; every step is a gfx950 kernel:
   render               stratified sampling (nerf_sample_stratified) -> fused coarse MLP ->
                        compositing (nerf_composite_fwd/bwd, autograd) -> importance sampling
                        + merge (nerf_sample_pdf) -> fused fine MLP -> compositing
-  render_accelerated   occupancy-grid march with early termination (nerf_march_*), a few
-                       host syncs per frame instead of one per t step
+  render_accelerated   occupancy-grid march with early termination (nerf_march_*): rounds of
+                       gather -> MLP -> composite sized on the device, one host check for live
+                       rays every 4 rounds (the reference syncs once per t step)
   raw2outputs / sample_pdf / world_to_grid_indices   the reference's helper signatures
 
 Randomness (perturb > 0) comes from counter-based Philox streams inside the kernels,

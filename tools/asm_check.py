@@ -32,7 +32,8 @@ def build_asm(tmp, kernels=None):
             f.write("#define NERF_MLP_DEVICE_ONLY\n")
             f.write(f'#include "{ROOT}/nerf-replication_amd/csrc/mlp.hip"\n')
             f.write(f"template __global__ void nerf::mlp::{k}{args[k[:3]]};\n")
-        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+        extra = os.environ.get("NERF_ASM_EXTRA", "").split()  # variant -D flags (tools/build_variants.sh)
+        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", *extra,
                                        f"-I{ROOT}/include", "--cuda-device-only", "-S", src, "-o",
                                        os.path.join(tmp, f"k{i}.s")], cwd=tmp, stdout=subprocess.DEVNULL,
                                       stderr=subprocess.DEVNULL))
