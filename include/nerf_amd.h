@@ -82,6 +82,22 @@ int nerf_composite_fwd(const float* raw, const float* z, const float* dirs, int 
 int nerf_composite_bwd(const float* raw, const float* z, const float* dirs, int dir_stride, int64_t R, int S,
                        int white_bkgd, const float* g_rgb, const float* g_depth, const float* g_acc, float* g_raw,
                        hipStream_t stream);
+/* The coarse pass's compositing and the importance sampling + merge that reads its weights, in one
+ * launch (volume_renderer.py:197-221; the weights handed over in registers): the outputs of
+ * nerf_composite_fwd (S = Sc <= 64; weights nullable) and of nerf_sample_pdf (z_fine, pts_fine),
+ * bit-identical to the two separate launches. */
+int nerf_composite_pdf(const float* raw, const float* z, const float* dirs, int dir_stride, int64_t R, int Sc,
+                       int white_bkgd, float* rgb, float* depth, float* acc, float* weights, int Ni, int det,
+                       const float* u_lin, const float* u, uint64_t seed, uint64_t offset, const float* rays,
+                       float* z_fine, float* pts_fine, hipStream_t stream);
+
+/* ---- (a10) loss: MSE(rgb_map_c, gt) + MSE(rgb_map_f, gt) (src/train/trainers/nerf.py:21-29) -----
+ * n = 3 R values.  fwd: out[3] = (loss_c, loss_f, loss_c + loss_f), one workgroup, fp64 sums in a
+ * fixed order; f nullable.  bwd: gc = (2/n) (c - gt) (g_lc + g_total), gf = (2/n) (f - gt) (g_lf +
+ * g_total) with device-scalar output grads (null = 0), ATen's rounding order. */
+int nerf_mse2_fwd(const float* c, const float* f, const float* gt, int64_t n, float* out, hipStream_t stream);
+int nerf_mse2_bwd(const float* c, const float* f, const float* gt, int64_t n, const float* g_lc, const float* g_lf,
+                  const float* g_total, float* gc, float* gf, hipStream_t stream);
 
 /* ---- (a4-a6) fused PE + NeRF MLP ------------------------------------------------------------
  * Replaces Network.forward / NeRF.forward (src/models/nerf/network.py:49-74, 171-192) with

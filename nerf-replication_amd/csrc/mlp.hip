@@ -328,7 +328,16 @@ __global__ void pack_kernel(ParamPtrs prm, UnitOffsets uo, char* out) {
 // ------------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void lds_void;
 
+// (NERF_DIAG_NO_DMA / NERF_DIAG_NO_STORE: diagnostic timing builds only -- the weight stream or
+// the training stores left out, results meaningless -- to price them in the kernels' time)
+#ifndef NERF_DIAG_NO_DMA
+#define NERF_DIAG_NO_DMA 0
+#endif
+#ifndef NERF_DIAG_NO_STORE
+#define NERF_DIAG_NO_STORE 0
+#endif
 __device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t lds_wave_base) {
+  if constexpr (NERF_DIAG_NO_DMA) return;
   uint32_t saved;  // m0 is reserved to the compiler: save and restore it around the DMA
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(saved) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_wave_base)) : "memory");
@@ -808,6 +817,7 @@ __host__ __device__ constexpr int64_t block_stride_kib(int ntiles, int ch) {
 #endif
 template <int OFF>
 __device__ __forceinline__ void store16(uint4* p, uint4 v) {
+  if constexpr (NERF_DIAG_NO_STORE) return;
   const u32x4 w = {v.x, v.y, v.z, v.w};
   if constexpr (NERF_STORE_POLICY == 1) {
     __builtin_nontemporal_store(w, (u32x4*)p + OFF / 16);

@@ -219,16 +219,15 @@ struct PdfArgs {
   int32_t* inds_out;     // [R, Ni] or null
 };
 
-__global__ void __launch_bounds__(256) sample_pdf_kernel(PdfArgs a) {
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= a.R) return;
-  const int l = lane_id();
+// one ray (one wave): zc = z of coarse sample l (l < Sc), wn = its weight of sample l + 1
+// (l < Sc - 2) -- from memory (sample_pdf_kernel) or from the compositing registers
+// (composite_pdf_kernel), the same fp32 values either way
+__device__ __forceinline__ void sample_pdf_ray(const PdfArgs& a, int64_t r, int l, float zc, float wn) {
   const int nb = a.Sc - 1;  // bins (z mids) and CDF entries
   const int nw = a.Sc - 2;  // pdf weights
-  const float zc = l < a.Sc ? a.z[r * a.Sc + l] : 0.f;
   const float zn = __shfl(zc, l + 1 < 64 ? l + 1 : 63, 64);
   const float bin = l < nb ? fmul(0.5f, fadd(zn, zc)) : 0.f;  // .5 * (z[1:] + z[:-1])
-  const float w = l < nw ? fadd(a.weights[r * a.Sc + l + 1], 1e-5f) : 0.f;
+  const float w = l < nw ? fadd(wn, 1e-5f) : 0.f;
   const float wsum = torch_row_sum(w, nw);  // the CPU torch.sum's order (common.h)
   const float pdf = l < nw ? fdiv(w, wsum) : 0.f;
   // cdf[0] = 0, cdf[k] = fp32(sum_{j<k} pdf_j) accumulated in double (torch CPU cumsum)
@@ -280,6 +279,15 @@ __global__ void __launch_bounds__(256) sample_pdf_kernel(PdfArgs a) {
       }
     }
   }
+}
+
+__global__ void __launch_bounds__(256) sample_pdf_kernel(PdfArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.R) return;
+  const int l = lane_id();
+  const float zc = l < a.Sc ? a.z[r * a.Sc + l] : 0.f;
+  const float wn = l < a.Sc - 2 ? a.weights[r * a.Sc + l + 1] : 0.f;
+  sample_pdf_ray(a, r, l, zc, wn);
 }
 
 // reference-signature form: sample_pdf(bins [R,nb], weights [R,nb-1], N, det) -> samples
@@ -355,10 +363,8 @@ struct CompArgs {
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 
 template <int SPL, bool BWD>
-__global__ void __launch_bounds__(256) composite_kernel(CompArgs a) {
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= a.R) return;
-  const int l = lane_id();
+__device__ __forceinline__ void composite_ray(const CompArgs& a, int64_t r, int l, float (&w_out)[SPL],
+                                              float (&z_out)[SPL]) {
   const int S = a.S;
   const float dx = a.dirs[r * a.dir_stride + 0], dy = a.dirs[r * a.dir_stride + 1],
               dz = a.dirs[r * a.dir_stride + 2];
@@ -403,6 +409,8 @@ __global__ void __launch_bounds__(256) composite_kernel(CompArgs a) {
     T[k] = (float)run;
     run *= (double)x[k];
     w[k] = fmul(alpha[k], T[k]);
+    w_out[k] = w[k];
+    z_out[k] = zs[k];
   }
   if (!BWD) {
     float sr = 0.f, sg = 0.f, sb = 0.f, sd = 0.f, sa = 0.f;
@@ -464,6 +472,26 @@ __global__ void __launch_bounds__(256) composite_kernel(CompArgs a) {
       }
     }
   }
+}
+
+template <int SPL, bool BWD>
+__global__ void __launch_bounds__(256) composite_kernel(CompArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.R) return;
+  float w[SPL], z[SPL];
+  composite_ray<SPL, BWD>(a, r, lane_id(), w, z);
+}
+
+// the coarse pass's compositing and the importance sampling + merge that reads its weights,
+// fused (volume_renderer.py:197-221): one wave per ray, the weights handed over in registers
+__global__ void __launch_bounds__(256) composite_pdf_kernel(CompArgs c, PdfArgs p) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= c.R) return;
+  const int l = lane_id();
+  float w[1], z[1];
+  composite_ray<1, false>(c, r, l, w, z);
+  const float wn = __shfl(w[0], l + 1 < 64 ? l + 1 : 63, 64);  // weight of sample l + 1
+  sample_pdf_ray(p, r, l, l < c.S ? z[0] : 0.f, l < c.S - 2 ? wn : 0.f);
 }
 
 }  // namespace nerf
@@ -555,6 +583,22 @@ int nerf_composite_fwd(const float* raw, const float* z, const float* dirs, int 
   NERF_REQUIRE(raw && z && dirs && rgb && depth && acc, "nerf_composite_fwd: null pointer");
   CompArgs a{raw, z, dirs, dir_stride, R, S, white_bkgd, rgb, depth, acc, weights, nullptr, nullptr, nullptr, nullptr};
   return composite_launch(a, false, stream);
+}
+
+int nerf_composite_pdf(const float* raw, const float* z, const float* dirs, int dir_stride, int64_t R, int Sc,
+                       int white_bkgd, float* rgb, float* depth, float* acc, float* weights, int Ni, int det,
+                       const float* u_lin, const float* u, uint64_t seed, uint64_t offset, const float* rays,
+                       float* z_fine, float* pts_fine, hipStream_t stream) {
+  NERF_REQUIRE(Sc >= 3 && Sc <= 64 && Ni >= 1 && Ni <= 128 && Sc + Ni <= 256 && R >= 0 && dir_stride >= 3,
+               "nerf_composite_pdf: need 3 <= Sc <= 64, 1 <= Ni <= 128 (got %d, %d)", Sc, Ni);
+  if (R == 0) return 0;
+  NERF_REQUIRE(raw && z && dirs && rgb && depth && acc && z_fine, "nerf_composite_pdf: null pointer");
+  NERF_REQUIRE(!det || u_lin, "nerf_composite_pdf: det needs the linspace table");
+  NERF_REQUIRE(!pts_fine || rays, "nerf_composite_pdf: pts_fine needs rays");
+  CompArgs c{raw, z, dirs, dir_stride, R, Sc, white_bkgd, rgb, depth, acc, weights, nullptr, nullptr, nullptr, nullptr};
+  PdfArgs p{z, nullptr, R, Sc, Ni, det, u_lin, u, seed, offset, rays, z_fine, pts_fine, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL(composite_pdf_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, stream, c, p);
+  return check_launch("nerf_composite_pdf");
 }
 
 int nerf_composite_bwd(const float* raw, const float* z, const float* dirs, int dir_stride, int64_t R, int S,

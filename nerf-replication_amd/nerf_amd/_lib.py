@@ -32,6 +32,10 @@ SIGNATURES = {
     "nerf_sample_pdf_bins": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _p, _p, _u64, _u64, _p, _p, _p, _p]),
     "nerf_composite_fwd": (_i32, [_p, _p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _p]),
     "nerf_composite_bwd": (_i32, [_p, _p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _p]),
+    "nerf_composite_pdf": (_i32, [_p, _p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p, _u64, _u64,
+                                  _p, _p, _p, _p]),
+    "nerf_mse2_fwd": (_i32, [_p, _p, _p, _i64, _p, _p]),
+    "nerf_mse2_bwd": (_i32, [_p, _p, _p, _i64, _p, _p, _p, _p, _p, _p]),
     "nerf_mlp_net_params": (_i64, []),
     "nerf_mlp_param_offset": (_i64, [_i32]),
     "nerf_mlp_packed_bytes": (_i64, [_i32, _i32]),

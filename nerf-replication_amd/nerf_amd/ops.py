@@ -312,6 +312,83 @@ def composite(raw: torch.Tensor, z: torch.Tensor, rays_d: torch.Tensor, white_bk
     return _Composite.apply(raw.reshape(z.shape[0], z.shape[1], 4), z, rays_d, white_bkgd)
 
 
+class _CompositePdf(torch.autograd.Function):
+    """The coarse compositing (differentiable in raw, as _Composite) fused with the importance
+    sampling + merge that reads its weights (no gradient: the reference detaches the samples,
+    volume_renderer.py:216)."""
+
+    @staticmethod
+    def forward(ctx, raw, z, rays_d, white, n_importance, det, seed, offset, rays):
+        raw, z = _f32c(raw, "raw"), _f32c(z, "z")
+        R, Sc = z.shape
+        keep, dptr, dstride = _dirs_view(rays_d)
+        dev = raw.device
+        rgb = torch.empty(R, 3, device=dev, dtype=torch.float32)
+        depth = torch.empty(R, device=dev, dtype=torch.float32)
+        acc = torch.empty(R, device=dev, dtype=torch.float32)
+        S = Sc + n_importance
+        z_fine = torch.empty(R, S, device=dev, dtype=torch.float32)
+        pts_fine = torch.empty(R, S, 3, device=dev, dtype=torch.float32)
+        rays = _f32c(rays.reshape(-1, 6), "rays")
+        u_lin = device_table("linspace", 0.0, 1.0, n_importance, dev) if det else None
+        # bytes per ray: raw 16 B + z 4 B per coarse sample, dir + ray; merged z + pts written
+        nbytes = R * (20 * Sc + 12 + 24 + 16 * S + 20)
+        with kernel_timer("composite_pdf", nbytes, detail=True):
+            check(lib().nerf_composite_pdf(ptr(raw), ptr(z), dptr, dstride, R, Sc, int(bool(white)), ptr(rgb),
+                                           ptr(depth), ptr(acc), None, int(n_importance), int(bool(det)), ptr(u_lin),
+                                           None, seed, offset, ptr(rays), ptr(z_fine), ptr(pts_fine),
+                                           stream_of(raw)), "nerf_composite_pdf")
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(raw, z, keep)
+        ctx.dptr, ctx.dstride, ctx.white = dptr, dstride, int(bool(white))
+        ctx.mark_non_differentiable(z_fine, pts_fine)
+        return rgb, depth, acc, z_fine, pts_fine
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_depth, g_acc, g_zf, g_pf):
+        return _Composite.backward(ctx, g_rgb, g_depth, g_acc, None)[:1] + (None,) * 8
+
+
+def composite_sample_pdf(raw: torch.Tensor, z: torch.Tensor, rays: torch.Tensor, white_bkgd: bool, n_importance: int,
+                         det: bool, seed: int = 0, offset: int = 0):
+    """composite (rgb, depth, acc of the coarse pass) + sample_pdf (merged z_fine, pts_fine) in one
+    launch: bit-identical to composite() then sample_pdf(z, weights, ..., rays=rays)."""
+    rays = rays.reshape(-1, 6)
+    rgb, depth, acc, z_fine, pts_fine = _CompositePdf.apply(raw.reshape(z.shape[0], z.shape[1], 4), z, rays[:, 3:6],
+                                                            white_bkgd, n_importance, det, seed, offset, rays)
+    return rgb, depth, acc, {"z_fine": z_fine, "pts_fine": pts_fine}
+
+
+class _Mse2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, c, f, gt):
+        c, gt = _f32c(c, "rgb_c"), _f32c(gt, "gt")
+        f = _f32c(f, "rgb_f") if f is not None else None
+        out = torch.empty(3, device=c.device, dtype=torch.float32)
+        check(lib().nerf_mse2_fwd(ptr(c), ptr(f), ptr(gt), c.numel(), ptr(out), stream_of(c)), "nerf_mse2_fwd")
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(c, f, gt)
+        ctx.has_f = f is not None
+        return out[0], out[1], out[2]
+
+    @staticmethod
+    def backward(ctx, g_lc, g_lf, g_total):
+        c, f, gt = ctx.saved_tensors
+        gc = torch.empty_like(c)
+        gf = torch.empty_like(f) if ctx.has_f else None
+        g = [None if t is None else t.reshape(1).to(torch.float32).contiguous() for t in (g_lc, g_lf, g_total)]
+        check(lib().nerf_mse2_bwd(ptr(c), ptr(f), ptr(gt), c.numel(), ptr(g[0]), ptr(g[1]), ptr(g[2]), ptr(gc),
+                                  ptr(gf), stream_of(c)), "nerf_mse2_bwd")
+        return gc, gf, None
+
+
+def mse_pair(rgb_c: torch.Tensor, rgb_f: Optional[torch.Tensor], gt: torch.Tensor):
+    """(MSE(rgb_c, gt), MSE(rgb_f, gt), their sum) -- nn.MSELoss twice and an add
+    (src/train/trainers/nerf.py:21-29) -- in one forward and one backward launch."""
+    gt = gt.reshape(rgb_c.shape)
+    return _Mse2.apply(rgb_c, rgb_f, gt)
+
+
 # --------------------------------------------------------------------------------------
 # MLP (autograd)
 # --------------------------------------------------------------------------------------

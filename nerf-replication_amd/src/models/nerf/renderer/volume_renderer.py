@@ -98,10 +98,16 @@ class Renderer:
                 o1, o2 = self._next_offsets()
                 z, pts, vd = ops.sample_stratified(rc, near, far, n_s, perturb, seed=self._seed, offset=o1)
             raw_c = self.net(pts, vd, "coarse")
-            rgb_c, dep_c, acc_c, w_c = self.raw2outputs(raw_c, z, rd, ta.raw_noise_std, white)
+            fused = n_i > 0 and float(ta.raw_noise_std) == 0.0 and n_s <= 64 and ta.get("fuse_composite_pdf", True)
+            if fused:  # raw2outputs + sample_pdf + merge in one launch (ops.composite_sample_pdf)
+                rgb_c, dep_c, acc_c, pdf = ops.composite_sample_pdf(raw_c, z, rc, white, n_i, det=not perturb,
+                                                                    seed=self._seed, offset=o2)
+            else:
+                rgb_c, dep_c, acc_c, w_c = self.raw2outputs(raw_c, z, rd, ta.raw_noise_std, white)
             ret = {"rgb_map_c": rgb_c, "depth_map_c": dep_c, "acc_map_c": acc_c}
             if n_i > 0:
-                pdf = ops.sample_pdf(z, w_c, n_i, det=not perturb, seed=self._seed, offset=o2, rays=rc)
+                if not fused:
+                    pdf = ops.sample_pdf(z, w_c, n_i, det=not perturb, seed=self._seed, offset=o2, rays=rc)
                 raw_f = self.net(pdf["pts_fine"], vd, "fine")
                 rgb_f, dep_f, acc_f, _ = self.raw2outputs(raw_f, pdf["z_fine"], rd, ta.raw_noise_std, white)
                 ret.update(rgb_map_f=rgb_f, depth_map_f=dep_f, acc_map_f=acc_f)

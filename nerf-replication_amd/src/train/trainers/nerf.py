@@ -7,6 +7,8 @@ at src.models.nerf.renderer.volume_renderer.
 """
 import torch.nn as nn
 
+from nerf_amd import ops
+
 from src.models.nerf.renderer.volume_renderer import Renderer
 
 
@@ -20,6 +22,10 @@ class NetworkWrapper(nn.Module):
     def forward(self, batch):
         ret = self.renderer.render(batch)
         gt = batch["rgbs"].reshape(-1, 3) if batch["rgbs"].dim() == 3 else batch["rgbs"]
+        if "rgb_map_f" in ret and ret["rgb_map_c"].is_cuda:
+            # both MSEs and their sum in one launch, the backward in one (ops.mse_pair)
+            loss_c, loss_f, total = ops.mse_pair(ret["rgb_map_c"], ret["rgb_map_f"], gt)
+            return ret, total, {"loss_c": loss_c, "loss_f": loss_f, "total_loss": total}
         loss_c = self.loss_fn(ret["rgb_map_c"], gt)
         stats = {"loss_c": loss_c}
         if "rgb_map_f" in ret:

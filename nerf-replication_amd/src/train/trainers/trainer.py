@@ -165,7 +165,8 @@ class Trainer:
         from nerf_amd import ops
         self.buckets.begin()
         output, loss, loss_stats = self.network(batch)
-        loss = loss.mean()
+        if loss.dim() > 0:  # (a 0-d loss is its own mean: no extra launch)
+            loss = loss.mean()
         optimizer.zero_grad()
         with ops.direct_grad():
             loss.backward()

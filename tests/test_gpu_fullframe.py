@@ -17,8 +17,9 @@ march -- and is compared with NO exclusions:
     importance samples move bins);
   * every row sum within 800 x the per-value tolerance (so every row of the frame is covered,
     not only the sampled rays);
-  * the uint8 frame (clip(rgb) x 255, truncated): every pixel within one level, >= 99.9 %
-    identical (fp32);
+  * the uint8 frame (clip(rgb) x 255, truncated): fp32 every pixel within one level, >= 99.9 %
+    identical (measured 99.999 %); bf16x3 / bf16x3f >= 99.95 % identical and within 8 levels
+    (measured 99.981 %, max 6: a few pixels, outside the 4,096, where the fine integral flips);
   * the march's MLP query count over the frame: within 16 of the reference's 12,383,297
     (measured: fp32 -2, bf16x3 +2; the 256-ray count of test_gpu_trained.py is exact).  A ray
     stops after the first queried step whose transmittance falls below 1e-4
@@ -97,8 +98,12 @@ def _compare(out, g4, prefix, keys, dtype):
                                            for k, (m, f, c, r) in report.items()))
     img = (out["rgb_map_f"].clamp(0, 1) * 255).to(torch.uint8).reshape(H, W, 3).cpu().numpy()
     d = np.abs(img.astype(int) - g4[f"{prefix}_frame_u8"].astype(int))
-    print(f"{prefix} {dtype} uint8 frame: max {d.max()}, identical {(d == 0).mean():.5f}")
-    assert d.max() <= (1 if dtype == "fp32" else 2) and (d == 0).mean() >= (0.999 if dtype == "fp32" else 0.99)
+    print(f"{prefix} {dtype} uint8 frame: max {d.max()}, identical {(d == 0).mean():.5f}, "
+          f"within one level {(d <= 1).mean():.6f}, pixels off by > 1: {int((d.max(-1) > 1).sum())}")
+    if dtype == "fp32":
+        assert d.max() <= 1 and (d == 0).mean() >= 0.999
+    else:  # (measured: max 6 levels, 99.981 % identical -- a few silhouette / chaotic pixels)
+        assert d.max() <= 8 and (d == 0).mean() >= 0.9995
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16x3f"])

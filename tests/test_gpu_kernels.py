@@ -736,3 +736,47 @@ def test_mlp_fwd_count_matches_fwd(cuda, ops, seeded_state, dtype):
             ref = ops.mlp(packer, pts[:n], vd, 1, di[:n], dtype) if n else torch.empty(0, 4, device=cuda)
         torch.testing.assert_close(raw[:n], ref, rtol=0, atol=0)
         assert bool(torch.isnan(raw[n:]).all())  # nothing past the device count is written
+
+
+@pytest.mark.parametrize("det", [True, False])
+def test_composite_pdf_fused_equals_separate(cuda, ops, det):
+    """ops.composite_sample_pdf (one launch: coarse compositing + importance sampling + merge,
+    the weights handed over in registers) is bit-identical to composite() then sample_pdf(),
+    forward and backward (volume_renderer.py:197-221)."""
+    g = torch.Generator().manual_seed(41)
+    R, Sc, Ni = 1000, 64, 128
+    o = torch.randn(R, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, 4.0])
+    d = torch.nn.functional.normalize(torch.randn(R, 3, generator=g), dim=-1) * 1.3
+    rays = torch.cat([o, d], 1).to(cuda)
+    z, _, _ = ops.sample_stratified(rays, 2.0, 6.0, Sc, not det, seed=5, offset=8)
+    raw = (torch.randn(R, Sc, 4, generator=g) * 2).to(cuda).requires_grad_(True)
+    raw2 = raw.detach().clone().requires_grad_(True)
+    rgb, dep, acc, w = ops.composite(raw, z, rays[:, 3:6], True)
+    pdf = ops.sample_pdf(z, w, Ni, det=det, seed=5, offset=9, rays=rays)
+    rgb2, dep2, acc2, pdf2 = ops.composite_sample_pdf(raw2, z, rays, True, Ni, det=det, seed=5, offset=9)
+    for a, b in ((rgb, rgb2), (dep, dep2), (acc, acc2), (pdf["z_fine"], pdf2["z_fine"]),
+                 (pdf["pts_fine"], pdf2["pts_fine"])):
+        assert torch.equal(a, b)
+    gr = torch.randn(R, 3, generator=g).to(cuda)
+    ((rgb * gr).sum() + dep.sum() + 0.5 * acc.sum()).backward()
+    ((rgb2 * gr).sum() + dep2.sum() + 0.5 * acc2.sum()).backward()
+    assert torch.equal(raw.grad, raw2.grad)
+
+
+def test_mse_pair_matches_torch(cuda, ops):
+    """ops.mse_pair = nn.MSELoss()(c, gt) + nn.MSELoss()(f, gt) (src/train/trainers/nerf.py:21-29):
+    the losses within fp32 rounding of torch's (fp64 sums here), the gradients of the total (and of
+    each loss) equal to torch's autograd."""
+    g = torch.Generator().manual_seed(42)
+    n = 4096
+    c0, f0, gt = (torch.rand(n, 3, generator=g).to(cuda) for _ in range(3))
+    c, f = c0.clone().requires_grad_(True), f0.clone().requires_grad_(True)
+    lc, lf, tot = ops.mse_pair(c, f, gt)
+    (tot + 0.25 * lc).backward()
+    c1, f1 = c0.clone().requires_grad_(True), f0.clone().requires_grad_(True)
+    rc, rf = torch.nn.functional.mse_loss(c1, gt), torch.nn.functional.mse_loss(f1, gt)
+    ((rc + rf) + 0.25 * rc).backward()
+    np.testing.assert_allclose([float(lc), float(lf), float(tot)], [float(rc), float(rf), float(rc + rf)], rtol=1e-6)
+    torch.testing.assert_close(c.grad, c1.grad, rtol=1e-6, atol=0)
+    torch.testing.assert_close(f.grad, f1.grad, rtol=1e-6, atol=0)
+    print(f"\nmse_pair grads bit-equal to torch's: c {torch.equal(c.grad, c1.grad)}, f {torch.equal(f.grad, f1.grad)}")
