@@ -446,10 +446,25 @@ __device__ __forceinline__ lds_cu4* lds_ptr(uint32_t byte_addr) {
 // input tile t, chunk c), in execution order.  A group's body is straight-line code over
 // it with the A operand (weights, LDS) prefetched PD steps ahead across unit boundaries
 // -- hipcc on its own keeps one ds_read in flight and waits lgkmcnt(0) before every MFMA.
-// DMA wave-instructions per wave for group g (fetch_group)
+//
+// LDS-DMA batching: 1 = one global_load_lds (1 KiB) per M0 setting; 4 = a wave copies blocks of
+// 4 consecutive chunks with one M0 and the instruction offsets 0 / 1 / 2 / 3 KiB (applied to the
+// global and the LDS address alike), 5 instructions per 4 KiB instead of ~28
+#ifndef NERF_DMA_BATCH
+#define NERF_DMA_BATCH 1
+#endif
+constexpr int DMA_BATCH = NERF_DMA_BATCH;
+static_assert(DMA_BATCH == 1 || DMA_BATCH == 4, "NERF_DMA_BATCH must be 1 or 4");
+// DMA units (of DMA_BATCH wave-instructions) per wave for group g (fetch_group)
+template <class P, int DIR, bool DENSITY>
+__host__ __device__ constexpr int group_dma_units(int g) {
+  const int nb = (GroupTable<DIR, DENSITY, P::CH>::t.g[g].nch + DMA_BATCH - 1) / DMA_BATCH;
+  return (nb + P::WAVES - 1) / P::WAVES;
+}
+// DMA wave-instructions per wave for group g
 template <class P, int DIR, bool DENSITY>
 __host__ __device__ constexpr int group_dma(int g) {
-  return (GroupTable<DIR, DENSITY, P::CH>::t.g[g].nch + P::WAVES - 1) / P::WAVES;
+  return group_dma_units<P, DIR, DENSITY>(g) * DMA_BATCH;
 }
 // vmcnt of the hand-off at the end of group g (group g + 1's DMA must have landed): the
 // wave's vector-memory ops younger than that DMA = the DMAs of groups g + 2 .. g + PF and
@@ -547,8 +562,8 @@ __host__ __device__ constexpr bool finished_in_group(int g, int u) {
 #define NERF_FINISH_PARTS_BF16 1
 #endif
 #ifndef NERF_FINISH_PARTS_BF3
-#define NERF_FINISH_PARTS_BF3 1
-#endif
+#define NERF_FINISH_PARTS_BF3 8  // with NERF_DMA_SPREAD_BF3 3: bf16x3 forward 1.70 -> 1.58 ms, training
+#endif                           // forward 1.97 -> 1.88, dX 1.73 -> 1.65 at 524,288 samples (r4)
 template <class P> __host__ __device__ constexpr int finish_parts() {
   return P::KIND == K_F32 ? NERF_FINISH_PARTS_F32 : P::KIND == K_BF16 ? NERF_FINISH_PARTS_BF16 : NERF_FINISH_PARTS_BF3;
 }
@@ -562,7 +577,7 @@ template <class P> __host__ __device__ constexpr int finish_parts() {
 #define NERF_DMA_SPREAD_BF16 0
 #endif
 #ifndef NERF_DMA_SPREAD_BF3
-#define NERF_DMA_SPREAD_BF3 0
+#define NERF_DMA_SPREAD_BF3 3
 #endif
 template <class P> __host__ __device__ constexpr int dma_spread() {
   return PF != 1 ? 0 : P::KIND == K_F32 ? NERF_DMA_SPREAD_F32 : P::KIND == K_BF16 ? NERF_DMA_SPREAD_BF16 : NERF_DMA_SPREAD_BF3;
@@ -588,7 +603,7 @@ __host__ __device__ constexpr int part_step(int g, int u, int p) {
 template <class P, int DIR, bool DENSITY>
 __host__ __device__ constexpr int dma_piece_step(int g, int i) {
   const int NS = group_steps<DIR, DENSITY, P::CH>(g);
-  const int NF = group_dma<P, DIR, DENSITY>(g + 1);
+  const int NF = group_dma_units<P, DIR, DENSITY>(g + 1);
   const int front = (NS + dma_spread<P>() - 1) / dma_spread<P>();
   return i * front / NF;
 }
@@ -598,7 +613,7 @@ __host__ __device__ constexpr int dma_piece_step(int g, int i) {
 template <class P, int DIR, bool DENSITY, class StoresFn>
 __host__ __device__ constexpr int handoff_vmcnt_spread(int g, StoresFn unit_stores) {
   if (g + 1 >= GroupTable<DIR, DENSITY, P::CH>::t.n) return 0;  // (the last group: no hand-off)
-  const int last = dma_piece_step<P, DIR, DENSITY>(g, group_dma<P, DIR, DENSITY>(g + 1) - 1);
+  const int last = dma_piece_step<P, DIR, DENSITY>(g, group_dma_units<P, DIR, DENSITY>(g + 1) - 1);
   const int NU = DIR == 0 ? NUNIT_FWD : NUNIT_BWD;
   int n = 0;
   for (int u = 0; u < NU; ++u) {
@@ -621,7 +636,7 @@ __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
   constexpr Group G = T.g[g];
   constexpr int PREV_U = g > 0 ? T.g[g - 1].u0 + T.g[g - 1].n - 1 : -1;  // previous group's last unit
   constexpr bool SPREAD = dma_spread<P>() > 0 && g + 1 < T.n;
-  constexpr int NF = SPREAD ? group_dma<P, DIR, DENSITY>(g + 1) : 0;
+  constexpr int NF = SPREAD ? group_dma_units<P, DIR, DENSITY>(g + 1) : 0;
   uint4 ring[PDP];
   sfor<(NS < PDP ? NS : PDP)>([&](auto kk) {
     constexpr int k = decltype(kk)::value;
@@ -665,33 +680,43 @@ __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
   });
 }
 
-// issue the DMA of group G into slot `slot`: every wave issues exactly NF wave-instructions
-// (the last chunk is re-copied by the surplus waves -- identical bytes), so the count a
-// later wait needs is a compile-time constant.
-template <class P, int C0, int NCH, bool LAUNDER = false>
-__device__ __forceinline__ void fetch_group(const uint4* gsrc, uint32_t slot_base, int wave, int lane) {
-  constexpr int NF = (NCH + P::WAVES - 1) / P::WAVES;
+// four consecutive 1 KiB chunks with one M0 (NERF_DMA_BATCH 4)
+__device__ __forceinline__ void glds16x4_asm(const void* gsrc, uint32_t lds_wave_base) {
+  if constexpr (NERF_DIAG_NO_DMA) return;
+  uint32_t saved;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\tglobal_load_lds_dwordx4 %1, off offset:1024\n\t"
+               "global_load_lds_dwordx4 %1, off offset:2048\n\tglobal_load_lds_dwordx4 %1, off offset:3072\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(saved) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_wave_base)) : "memory");
+}
+
+// DMA unit i of a wave for a group of NCH chunks starting at chunk C0 into slot `slot_base`:
+// every wave issues exactly group_dma_units units (the last chunk / block is re-copied by the
+// surplus waves -- identical bytes), so the count a later wait needs is a compile-time constant
+template <class P, int C0, int NCH, int I, bool LAUNDER = false>
+__device__ __forceinline__ void fetch_piece(const uint4* gsrc, uint32_t slot_base, int wave, int lane) {
   if constexpr (LAUNDER) {  // (persistent forward: the chunk indices are recomputed per group, not
     uint32_t w = wave;      // CSE'd across the groups and held -- spilled -- across the block loop)
     settle(w);
     wave = (int)w;
   }
-#pragma unroll
-  for (int i = 0; i < NF; ++i) {
-    const int k = cmin(wave + P::WAVES * i, NCH - 1);
+  if constexpr (DMA_BATCH == 1) {
+    const int k = cmin(wave + P::WAVES * I, NCH - 1);
     glds16_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
+  } else {
+    static_assert(NCH >= 4, "a DMA block needs 4 chunks");
+    constexpr int NB = (NCH + 3) / 4;
+    const int b = cmin(wave + P::WAVES * I, NB - 1);
+    const int k = cmin(4 * b, NCH - 4);  // (the last block overlaps its predecessor: same bytes)
+    glds16x4_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
   }
 }
-// the i-th of fetch_group's NF wave-instructions alone (the DMA spread over a group body)
-template <class P, int C0, int NCH, int I, bool LAUNDER = false>
-__device__ __forceinline__ void fetch_piece(const uint4* gsrc, uint32_t slot_base, int wave, int lane) {
-  if constexpr (LAUNDER) {
-    uint32_t w = wave;
-    settle(w);
-    wave = (int)w;
-  }
-  const int k = cmin(wave + P::WAVES * I, NCH - 1);
-  glds16_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
+// issue the whole DMA of group G into slot `slot` (group_dma_units units per wave)
+template <class P, int C0, int NCH, bool LAUNDER = false>
+__device__ __forceinline__ void fetch_group(const uint4* gsrc, uint32_t slot_base, int wave, int lane) {
+  constexpr int NU = ((NCH + DMA_BATCH - 1) / DMA_BATCH + P::WAVES - 1) / P::WAVES;
+  sfor<NU>([&](auto ii) { fetch_piece<P, C0, NCH, decltype(ii)::value, LAUNDER>(gsrc, slot_base, wave, lane); });
 }
 
 

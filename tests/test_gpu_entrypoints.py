@@ -58,8 +58,9 @@ def _run(args, cwd, timeout=600):
     return r.stdout
 
 
-# occupied fraction of the seeded 300-step net's res-128 bake (occupancy_grid.py:65-70)
-OCC_BAND = (0.001, 0.9)
+# occupied fraction of the seeded 300-step net's res-128 bake (occupancy_grid.py:65-70):
+# measured 0.11174 (234,334 cells); the band is +-15 %
+OCC_BAND = (0.095, 0.1285)
 
 
 def test_train_grid_evaluate_workflow(cuda, tmp_path):

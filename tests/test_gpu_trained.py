@@ -46,11 +46,13 @@ MAXERR = {"fp32": 1e-4, "bf16x3": 2e-3, "bf16x3f": 2e-3, "bf16": 3e-2}  # bound 
 # emulation of the bf16 kernels' rounding predicts (tools/precision_rank.py b:b: 0.737 / 0.310,
 # 0.365 / 0.089), so the kernels are pinned to their rounding model (test_gpu_kernels.py
 # BF16_EMU_TOL) and these bounds only hold the end-to-end gradient to what that model gives
-GRAD_REL = {"fp32": 1e-4, "bf16x3": 2e-3, "bf16x3f": 3e-2, "bf16": 1.0}
+GRAD_REL = {"fp32": 1e-4, "bf16x3": 2e-3, "bf16x3f": 6e-3, "bf16": 1.0}
 BF16_GRAD_L2 = {"grad64": 0.5, "grad4096": 0.15}
 # bf16x3f: the bf16x3 forward (so the same ReLU branches and samples as the reference, to ~1e-5)
-# with the bf16 backward: its gradients carry only the backward's own rounding
-BF16X3F_GRAD_L2 = {"grad64": 3e-2, "grad4096": 3e-2}
+# with the bf16 backward: its gradients carry only the backward's own rounding (measured: largest
+# entry error 3.6e-3 / 2.9e-3 of the tensor's largest, relative L2 2.1e-3 / 9.4e-4 for 64 / 4096
+# rays -- 200-350x closer than the bf16 tier's 0.74 / 0.31)
+BF16X3F_GRAD_L2 = {"grad64": 4e-3, "grad4096": 2e-3}
 
 
 @pytest.fixture(scope="module")

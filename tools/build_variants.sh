@@ -15,6 +15,7 @@ while [ $# -gt 1 ]; do
   rm -rf $B
   if [ -n "$ONLY" ]; then
     cp -rp $ROOT/build/nerf_amd $B
+    touch $B/*.o  # (newer than any edited source: only the listed objects are rebuilt)
     for o in $ONLY; do rm -f $B/$o.o; done
   fi
   make -C $CS -j8 BUILD=$B OUT=$ROOT/variants/$name.so EXTRA="$defs" > /tmp/nerf_var_$name.log 2>&1 || { tail -20 /tmp/nerf_var_$name.log; exit 1; }

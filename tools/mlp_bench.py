@@ -96,6 +96,8 @@ def load_handle(path):
     import ctypes
     h = ctypes.CDLL(os.path.abspath(path))
     for name, (res, argt) in _lib.SIGNATURES.items():
+        if not hasattr(h, name):  # (an older build: only the MLP entry points are used here)
+            continue
         fn = getattr(h, name)
         fn.restype = res
         fn.argtypes = argt
