@@ -63,7 +63,7 @@ def kernel_prec(kernel: str, dtype: str) -> str:
 
 
 # HBM-bound sampling / compositing kernels; ops.py counts their algorithmic bytes per launch
-STREAM_KERNELS = ("raygen", "sample_stratified", "sample_pdf", "composite_fwd", "composite_bwd")
+STREAM_KERNELS = ("raygen", "sample_stratified", "sample_pdf", "composite_pdf", "composite_fwd", "composite_bwd")
 
 
 def parse(argv=None):

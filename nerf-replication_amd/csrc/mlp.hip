@@ -556,11 +556,11 @@ __host__ __device__ constexpr bool finished_in_group(int g, int u) {
 // MFMAs).  With NP parts, part p (register pairs [8p/NP, 8(p+1)/NP)) is issued FINISH_DELAY + p
 // steps into the next unit, clamped to that unit's last step; the last part stores.
 #ifndef NERF_FINISH_PARTS_F32
-#define NERF_FINISH_PARTS_F32 1
+#define NERF_FINISH_PARTS_F32 1  // (fp32: 8 parts + spread DMA measured 4.88 -> 5.05 ms, training forward)
 #endif
 #ifndef NERF_FINISH_PARTS_BF16
-#define NERF_FINISH_PARTS_BF16 1
-#endif
+#define NERF_FINISH_PARTS_BF16 4  // with NERF_DMA_SPREAD_BF16 3: bf16 inference forward 0.517 -> 0.488 ms,
+#endif                            // dX 0.619 -> 0.609 at 524,288 samples (r4; 8 parts: no gain)
 #ifndef NERF_FINISH_PARTS_BF3
 #define NERF_FINISH_PARTS_BF3 8  // with NERF_DMA_SPREAD_BF3 3: bf16x3 forward 1.70 -> 1.58 ms, training
 #endif                           // forward 1.97 -> 1.88, dX 1.73 -> 1.65 at 524,288 samples (r4)
@@ -574,7 +574,7 @@ template <class P> __host__ __device__ constexpr int finish_parts() {
 #define NERF_DMA_SPREAD_F32 0
 #endif
 #ifndef NERF_DMA_SPREAD_BF16
-#define NERF_DMA_SPREAD_BF16 0
+#define NERF_DMA_SPREAD_BF16 3
 #endif
 #ifndef NERF_DMA_SPREAD_BF3
 #define NERF_DMA_SPREAD_BF3 3

@@ -403,6 +403,8 @@ _PARAM_GENERATION = [0]
 _DIRECT_GRAD = [0]
 # dW partial sums reduced in a fixed order (bit-reproducible gradients) instead of fp32 atomics
 DETERMINISTIC_DW = True
+# samples per backward chunk, by backward precision (a multiple of 256; absent = one launch)
+BWD_CHUNK = {BF16: 262144}
 
 
 class direct_grad:
@@ -550,14 +552,25 @@ class _MLP(torch.autograd.Function):
         grad = direct if direct is not None else torch.zeros(lib().nerf_mlp_net_params(), device=dev,
                                                               dtype=torch.float32)
         s = stream_of(g_raw)
-        with kernel_timer("mlp_bwd_dx", ctx.M):
-            check(lib().nerf_mlp_bwd_dx(ptr(ctx.packed_bwd), ctx.dtype, ptr(g_raw), ctx.M, ptr(ctx.masks), ptr(dz), s),
-                  "nerf_mlp_bwd_dx")
-        ws = torch.empty(lib().nerf_mlp_dw_workspace_bytes(ctx.dtype, ctx.M), dtype=torch.uint8, device=dev) \
+        L = lib()
+        # the backward in chunks of BWD_CHUNK samples (dX then dW per chunk; the stores are
+        # block-major, so a chunk is a contiguous byte range of each): bf16 backward 2.52 -> 2.31 ms
+        # for a 786,432-sample fine launch, fp32 none (tools/mlp_bench.py --chunks)
+        C = BWD_CHUNK.get(pack_code(ctx.dtype, 1), ctx.M)
+        C = ctx.M if C >= ctx.M else C
+        ws = torch.empty(L.nerf_mlp_dw_workspace_bytes(ctx.dtype, C), dtype=torch.uint8, device=dev) \
             if DETERMINISTIC_DW else None
-        with kernel_timer("mlp_bwd_dw", ctx.M):
-            check(lib().nerf_mlp_bwd_dw_ws(ctx.dtype, ctx.M, ptr(ctx.act), ptr(dz), ptr(grad), ptr(ws), s),
-                  "nerf_mlp_bwd_dw")
+        z_blk, a_blk = L.nerf_mlp_dz_bytes(ctx.dtype, 256) // 8, L.nerf_mlp_act_bytes(ctx.dtype, 256) // 8
+        m_blk = L.nerf_mlp_mask_bytes(256) // 8
+        for s0 in range(0, ctx.M, C):
+            m, b0 = min(C, ctx.M - s0), s0 // 32
+            with kernel_timer("mlp_bwd_dx", m):
+                check(L.nerf_mlp_bwd_dx(ptr(ctx.packed_bwd), ctx.dtype, g_raw.data_ptr() + 16 * s0, m,
+                                        ctx.masks.data_ptr() + b0 * m_blk, dz.data_ptr() + b0 * z_blk, s),
+                      "nerf_mlp_bwd_dx")
+            with kernel_timer("mlp_bwd_dw", m):
+                check(L.nerf_mlp_bwd_dw_ws(ctx.dtype, m, ctx.act.data_ptr() + b0 * a_blk, dz.data_ptr() + b0 * z_blk,
+                                           ptr(grad), ptr(ws), s), "nerf_mlp_bwd_dw")
         ctx.act = ctx.masks = None
         # the net's data-parallel bucket starts after its last pending chunk's dW only
         ctx.packer.backward_done(grad if direct is not None else None)

@@ -39,7 +39,10 @@ def test_mlp_kernels_handoffs_and_registers(capsys):
         # the persistent inference forwards (PERSIST = true) re-run the straight-line body per sample
         # block: a few hundred bytes of spills, reloaded ~70 times per block of ~40k instructions
         persist = re.search(r"Lb0ELb0ELb1ELb0EE", m.group(2)) is not None
+        # the bf16 training forward with 4 finish parts + spread DMA (round 4): 88 B, measured
+        # 0.662 ms against 0.663 without the parts (profiles/r4/pipeline_experiments.json)
         assert (("fwd_kernelINS0_4PF32ELb1ELb0" in m.group(2) and int(m.group(1)) <= 24)
+                or ("fwd_kernelINS0_5PBF16ELb1ELb0" in m.group(2) and int(m.group(1)) <= 96)
                 or (persist and int(m.group(1)) <= 320)), "\n" + out
     assert re.search(r"ok  _ZN4nerf3mlp10fwd_kernelINS0_5PBF16ELb0ELb0ELb1E", out), "\n" + out
     for name in ("fwd_kernelINS0_5PBF16ELb1ELb0", "fwd_kernelINS0_4PF32ELb1ELb0", "dx_kernelINS0_4PF32",

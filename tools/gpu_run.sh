@@ -13,6 +13,7 @@
 #   pmc=DTYPE        PMC passes (traffic + stall counters) of the MLP kernels -> gpurun_out/pmc_DTYPE/
 #   mlp=ARGS         tools/mlp_bench.py ARGS (comma-free; use + for spaces)
 #   march=DTYPE      tools/march_bench.py --dtype DTYPE
+#   traffic=DTYPE    PMC FETCH_SIZE / WRITE_SIZE passes of a short bench -> gpurun_out/traffic_DTYPE.json
 # Logs go to gpurun_out/<step>.log.
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -45,6 +46,11 @@ for step in "$@"; do
           run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- \
             python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-eager-baseline ;;
     pmc=*) run "pmc_${step#pmc=}" 900 bash tools/gpu_pmc_mlp.sh "${step#pmc=}" ;;
+    traffic=*) dt=${step#traffic=}; rm -rf gpurun_out/tr_$dt
+          B="python3 bench.py --dtype $dt --no-second --no-render --no-cpu-baseline --no-eager-baseline --steps 3 --warmup 1 --detail-steps 2"
+          run "trF_$dt" 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/tr_$dt/F -o p --output-format csv -- $B
+          run "trW_$dt" 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/tr_$dt/W -o p --output-format csv -- $B
+          python3 tools/pmc_traffic.py gpurun_out/tr_$dt/F/p_counter_collection.csv gpurun_out/tr_$dt/W/p_counter_collection.csv $dt > gpurun_out/traffic_$dt.json || exit 1 ;;
     mlp=*) args=${step#mlp=}; nm=$((nm + 1)); run "mlp$nm" 600 python3 tools/mlp_bench.py ${args//+/ } ;;
     march=*) run "march_${step#march=}" 400 python3 tools/march_bench.py --dtype "${step#march=}" ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -30,6 +30,10 @@ def main():
     ap.add_argument("--lib", default=None, help="alternative build of libnerf_amd.so (kernel experiments)")
     ap.add_argument("--libs", default=None, help="comma-separated builds, timed in interleaved rounds in this process")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--chunks", default=None,
+                    help="comma-separated sample counts: time the backward (dX then dW) run per chunk of that many "
+                         "samples, so dW reads each chunk's dZ soon after dX wrote it (Infinity Cache, 256 MiB), "
+                         "against the one-launch backward")
     args = ap.parse_args()
     if args.lib:
         _lib.LIB_PATH = os.path.abspath(args.lib)
@@ -74,6 +78,9 @@ def main():
         "pack": pack,
     }
     out = {"M": M, "dtype": args.dtype}
+    if args.chunks:
+        kern["fwd_train"]()  # (act and masks of a real forward)
+        return chunked_backward(args, L, dt, M, pb, d_raw, masks, act, dz, grad, s)
     for name, fn in kern.items():
         fn()
         torch.cuda.synchronize()
@@ -89,6 +96,50 @@ def main():
         if name in FLOP:
             ent["tflops"] = round(FLOP[name] * M / (ms * 1e-3) / 1e12, 1)
         out[name] = ent
+    print(json.dumps(out), flush=True)
+
+
+def chunked_backward(args, L, dt, M, pb, d_raw, masks, act, dz, grad, s):
+    """dX + dW (deterministic workspace form) over the whole M, against the same work in chunks of C
+    samples (C a multiple of 256: the stores are block-major, a chunk is a contiguous byte range of
+    every store).  Prints ms per variant, and whether the chunked gradient equals the one-launch
+    one (it need not be bit-equal: the per-item partial sums add in another order)."""
+    z_blk = L.nerf_mlp_dz_bytes(dt, 256) // 8    # bytes per 32-sample block of each store
+    a_blk = L.nerf_mlp_act_bytes(dt, 256) // 8
+    m_blk = L.nerf_mlp_mask_bytes(256) // 8
+    sizes = [M] + [int(c) for c in args.chunks.split(",")]
+    ws = torch.empty(L.nerf_mlp_dw_workspace_bytes(dt, M), dtype=torch.uint8, device=act.device)
+    out = {"M": M, "dtype": args.dtype, "ms": {}}
+    grads = {}
+
+    def run(C):
+        for s0 in range(0, M, C):
+            m = min(C, M - s0)
+            b0 = s0 // 32
+            check(L.nerf_mlp_bwd_dx(ptr(pb), dt, d_raw.data_ptr() + s0 * 16, m, masks.data_ptr() + b0 * m_blk,
+                                    dz.data_ptr() + b0 * z_blk, s), "dx")
+            check(L.nerf_mlp_bwd_dw_ws(dt, m, act.data_ptr() + b0 * a_blk, dz.data_ptr() + b0 * z_blk, ptr(grad),
+                                       ptr(ws), s), "dw")
+    for C in sizes:
+        assert C % 256 == 0
+        grad.zero_()
+        run(C)
+        torch.cuda.synchronize()
+        grads[C] = grad.clone()
+        times = []
+        for _ in range(args.rounds):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(args.reps):
+                run(C)
+            b.record()
+            torch.cuda.synchronize()
+            times.append(a.elapsed_time(b) / args.reps)
+        times.sort()
+        out["ms"][str(C)] = round(times[len(times) // 2], 4)
+    g0 = grads[M]
+    out["max_rel_diff_vs_one_launch"] = {str(C): float((grads[C] - g0).abs().max() / g0.abs().max()) for C in sizes[1:]}
     print(json.dumps(out), flush=True)
 
 

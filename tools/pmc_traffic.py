@@ -29,6 +29,7 @@ LABELS = {
     "raygen_kernel(": "raygen",
     "stratified_kernel(": "sample_stratified",
     "sample_pdf_kernel(": "sample_pdf",
+    "composite_pdf_kernel(": "composite_pdf",
     "composite_kernel<1, false>": "composite_fwd",
     "composite_kernel<3, false>": "composite_fwd",
     "composite_kernel<1, true>": "composite_bwd",
