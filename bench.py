@@ -128,16 +128,22 @@ def launch_ranks(gpus: int, argv) -> int:
     return proc.wait()
 
 
-def pmc_traffic(kernel, dtype):
+def pmc_traffic(kernel, dtype, samples=None):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/r*/traffic.json, written by tools/pmc_traffic.py from rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this bench), or (None, None)."""
+    FETCH_SIZE / WRITE_SIZE passes of this bench), or (None, None).  An MLP kernel's bytes are
+    proportional to its samples: with ``samples`` (this run's samples per launch) they are
+    scaled from the summary's ``mlp_samples_per_launch`` (the PMC run's; 524,288 = the mean of
+    the coarse and the fine launch when each backward is one launch)."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic*.json")), reverse=True):
         with open(path) as f:
             d = json.load(f)
         if d.get("dtype") == dtype and kernel in d.get("kernels", {}):
-            return d["kernels"][kernel]["traffic_bytes"], os.path.relpath(path, ROOT)
+            t = d["kernels"][kernel]["traffic_bytes"]
+            if samples is not None and kernel.startswith("mlp_"):
+                t = t * samples / d.get("mlp_samples_per_launch", 524288)
+            return t, os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -268,12 +274,12 @@ def mlp_roofline(k, n, ms, units, dtype):
             "avg_launch_ms": round(avg_ms, 4)}
 
 
-def hbm_roofline(k, n, ms, dtype):
+def hbm_roofline(k, n, ms, dtype, samples=None):
     """The same launch against HBM: PMC bytes per launch (the newest committed traffic summary
     for this dtype, profiles/r*/traffic_*.json) / its mean HIP-event duration, against 8 TB/s.
     The bf16 training kernels move their stored tiles at 4.6-5.7 TB/s (the ~6.3 TB/s a copy
     reaches, MI355X_MICROARCH.md): HBM, not the MFMA, bounds them."""
-    traffic, src = pmc_traffic(k, dtype)
+    traffic, src = pmc_traffic(k, dtype, samples)
     if traffic is None:
         return None
     ach = traffic / (ms / n * 1e-3) / 1e9
@@ -324,7 +330,7 @@ def measure_training(args, world, rank, device, dtype):
     # dominant kernel: largest total device time among the MLP kernels
     name, (n_launch, ms, units) = max(ktimes.items(), key=lambda kv: kv[1][1])
     esize = 2 if dtype in ("bf16", "bf16x3f") else 4
-    traffic, traffic_src = pmc_traffic(name, dtype)
+    traffic, traffic_src = pmc_traffic(name, dtype, units / n_launch)
     store_bytes = STORE_ROWS * esize * units / n_launch
     io_bytes = MLP_IO_BYTES * units / n_launch
     roofline = dict(kernel=name, **mlp_roofline(name, n_launch, ms, units, dtype), traffic=traffic,
@@ -332,7 +338,7 @@ def measure_training(args, world, rank, device, dtype):
                     store_bytes_per_launch=store_bytes, mlp_io_bytes_per_launch=io_bytes,
                     traffic_vs_mlp_io=None if traffic is None else round(traffic / io_bytes, 1))
     kt = {k: {"launches": n, "avg_ms": round(m / n, 4), "roofline": mlp_roofline(k, n, m, u, dtype),
-              "hbm": hbm_roofline(k, n, m, dtype)} for k, (n, m, u) in ktimes.items()}
+              "hbm": hbm_roofline(k, n, m, dtype, u / n)} for k, (n, m, u) in ktimes.items()}
     return value, elapsed / args.steps * 1e3, roofline, kt, train_stream, (cfg, net, ds), dist_info
 
 

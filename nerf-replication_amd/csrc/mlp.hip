@@ -873,6 +873,15 @@ __device__ __forceinline__ uint4* mask_slot(void* masks, int64_t wblock, int grp
   return (uint4*)masks + (wblock * MASK_GROUPS + grp) * 64 + lane;
 }
 
+// NERF_KEEP_PE_BF3: the bf16x3 forward holds its position-encoding tiles X from L0 to the
+// skip input of L5 instead of recomputing them there (its f64-reduced polynomial sin/cos):
+// bit-identical, inference forward 1.526 -> 1.498 ms, bf16x3f training forward 1.688 -> 1.668,
+// bf16x3 1.872 -> 1.845 at 524,288 samples (r4).  fp32 / bf16 recompute (their register budgets)
+#ifndef NERF_KEEP_PE_BF3
+#define NERF_KEEP_PE_BF3 1
+#endif
+template <class P> __host__ __device__ constexpr bool keep_pe() { return P::KIND == K_BF16X3 && NERF_KEEP_PE_BF3; }
+
 // ------------------------------------------------------------------------------------
 // forward: one wave = 32 samples through all 11 layers; activations stay in registers
 // (feature-major accumulator layout = the next layer's B operand).
@@ -1043,7 +1052,7 @@ struct FwdWave {
   }
   template <int u> __device__ __forceinline__ void init(f32x16& acc) {
     constexpr int L = fwd_unit_layer(u), n = u - fwd_unit_first(L);
-    if constexpr (L == L5 && n == 0) {  // PE recomputed for the skip instead of held through L1..L4
+    if constexpr (L == L5 && n == 0 && !keep_pe<P>()) {  // PE recomputed for the skip instead of held through L1..L4
       settle(px);  // opaque to hipcc: it would otherwise CSE this with the L0 tiles and hold them
       settle(py);
       settle(pz);

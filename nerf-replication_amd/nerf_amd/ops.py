@@ -14,8 +14,10 @@ Reference interfaces mirrored (echo636/nerf-replication):
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as _ctypes
 import functools
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -403,8 +405,35 @@ _PARAM_GENERATION = [0]
 _DIRECT_GRAD = [0]
 # dW partial sums reduced in a fixed order (bit-reproducible gradients) instead of fp32 atomics
 DETERMINISTIC_DW = True
-# samples per backward chunk, by backward precision (a multiple of 256; absent = one launch)
-BWD_CHUNK = {BF16: 262144}
+# samples per backward chunk, by backward precision (a multiple of 256; absent = one launch).
+# None by default: in the whole training step (tools/step_ab.py, interleaved) 262,144-sample
+# chunks were slower for bf16 (4.57 vs 4.53 ms/step) and bf16x3f (6.53 vs 6.49), although the
+# backward alone was faster chunked (tools/mlp_bench.py --chunks)
+BWD_CHUNK = {}
+
+
+# inside direct_grad(), with NERF_DW_STREAM=1: the dW launches run on a second stream (per
+# device), each after its chunk's dX, so the next dX -- the same net's next chunk, or the other
+# net's backward -- overlaps the dW's dZ stream; direct_grad's exit joins it.  Bit-identical;
+# off by default: in the whole step (tools/step_ab.py) bf16 4.53 -> 4.44 ms but bf16x3f 6.49 ->
+# 6.53 -- the overlap is only the dW's work-item tail (a dX workgroup needs a whole CU's LDS)
+DW_STREAM = os.environ.get("NERF_DW_STREAM", "0") == "1"
+_DW_STREAMS = {}
+_DW_PENDING = []  # (device, event recorded on its dW stream after the last enqueued dW)
+
+
+def dw_stream(dev: torch.device) -> torch.cuda.Stream:
+    st = _DW_STREAMS.get(dev.index)
+    if st is None:
+        st = _DW_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    return st
+
+
+def dw_join() -> None:
+    """The current stream waits for every dW enqueued on the dW streams (a no-op when none is)."""
+    while _DW_PENDING:
+        dev, ev = _DW_PENDING.pop()
+        torch.cuda.current_stream(dev).wait_event(ev)
 
 
 class direct_grad:
@@ -412,7 +441,8 @@ class direct_grad:
     are views of one flat buffer (FusedAdam): inside it the dW kernel adds straight into
     ``.grad`` (no zero-filled temporary, no 24 autograd accumulations) and autograd receives
     None for the parameters.  Outside it (``torch.autograd.grad``, hooks, a non-flat
-    optimizer) the MLP backward returns ordinary gradients to autograd."""
+    optimizer) the MLP backward returns ordinary gradients to autograd.  On exit the compute
+    stream waits for the dW stream (DW_STREAM): every later use of ``.grad`` sees it whole."""
 
     def __enter__(self):
         _DIRECT_GRAD[0] += 1
@@ -420,6 +450,7 @@ class direct_grad:
 
     def __exit__(self, *exc):
         _DIRECT_GRAD[0] -= 1
+        dw_join()
         return False
 
 
@@ -554,26 +585,39 @@ class _MLP(torch.autograd.Function):
         s = stream_of(g_raw)
         L = lib()
         # the backward in chunks of BWD_CHUNK samples (dX then dW per chunk; the stores are
-        # block-major, so a chunk is a contiguous byte range of each): bf16 backward 2.52 -> 2.31 ms
-        # for a 786,432-sample fine launch, fp32 none (tools/mlp_bench.py --chunks)
+        # block-major, so a chunk is a contiguous byte range of each); off by default (BWD_CHUNK)
         C = BWD_CHUNK.get(pack_code(ctx.dtype, 1), ctx.M)
         C = ctx.M if C >= ctx.M else C
         ws = torch.empty(L.nerf_mlp_dw_workspace_bytes(ctx.dtype, C), dtype=torch.uint8, device=dev) \
             if DETERMINISTIC_DW else None
         z_blk, a_blk = L.nerf_mlp_dz_bytes(ctx.dtype, 256) // 8, L.nerf_mlp_act_bytes(ctx.dtype, 256) // 8
         m_blk = L.nerf_mlp_mask_bytes(256) // 8
+        side = dw_stream(dev) if direct is not None and DW_STREAM and dev.type == "cuda" else None
         for s0 in range(0, ctx.M, C):
             m, b0 = min(C, ctx.M - s0), s0 // 32
             with kernel_timer("mlp_bwd_dx", m):
                 check(L.nerf_mlp_bwd_dx(ptr(ctx.packed_bwd), ctx.dtype, g_raw.data_ptr() + 16 * s0, m,
                                         ctx.masks.data_ptr() + b0 * m_blk, dz.data_ptr() + b0 * z_blk, s),
                       "nerf_mlp_bwd_dx")
-            with kernel_timer("mlp_bwd_dw", m):
-                check(L.nerf_mlp_bwd_dw_ws(ctx.dtype, m, ctx.act.data_ptr() + b0 * a_blk, dz.data_ptr() + b0 * z_blk,
-                                           ptr(grad), ptr(ws), s), "nerf_mlp_bwd_dw")
+            if side is not None:  # this chunk's dW after its dX, on the dW stream
+                side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                with kernel_timer("mlp_bwd_dw", m):
+                    check(L.nerf_mlp_bwd_dw_ws(ctx.dtype, m, ctx.act.data_ptr() + b0 * a_blk,
+                                               dz.data_ptr() + b0 * z_blk, ptr(grad), ptr(ws),
+                                               side.cuda_stream if side is not None else s), "nerf_mlp_bwd_dw")
+        if side is not None:
+            for t in (ctx.act, dz, ws):  # (freed by this function; the dW stream still reads them)
+                if t is not None:
+                    t.record_stream(side)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            _DW_PENDING.append((dev, ev))
         ctx.act = ctx.masks = None
-        # the net's data-parallel bucket starts after its last pending chunk's dW only
-        ctx.packer.backward_done(grad if direct is not None else None)
+        # the net's data-parallel bucket starts after its last pending chunk's dW only (with the
+        # dW stream current, the bucket's collective is enqueued behind the dW)
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            ctx.packer.backward_done(grad if direct is not None else None)
         if direct is not None:
             return nones + (None,) * len(params)
         out, off = [], 0

@@ -160,3 +160,50 @@ def test_psnr_fp32_vs_bf16_training(cuda, steps, every):
     # config-3 runs put bf16 +0.23 dB from fp32, inside its own 0.47 dB seed-to-seed spread
     assert abs(summary["mean_delta_db"]) <= 0.8, summary
     assert abs(summary["mean_delta_db_bf16x3"]) <= 0.5, summary
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3f", "bf16"])
+def test_backward_scheduling_knobs(cuda, dtype):
+    """The MLP backward's opt-in schedules (nerf_amd/ops.py) on the production step's
+    forward_backward (4096 rays of the config-3 batch, trained weights, direct dW into the flat
+    .grad): the dW stream (NERF_DW_STREAM, every dW on a second stream after its dX) gives the
+    one-stream gradient bit for bit; the chunked backward (BWD_CHUNK, dX + dW per 262,144
+    samples) the same gradient up to the order of the dW partial sums (relative 1e-5 of each
+    tensor's largest entry; measured ~5e-7, tools/mlp_bench.py --chunks)."""
+    from nerf_amd import ops
+    from src.config import cfg
+    from src.models.nerf.network import Network
+    from src.train.optimizer import make_optimizer
+    from src.train.trainers.make_trainer import make_trainer
+    g2 = np.load(os.path.join(HERE, "golden", "golden_v2.npz"), allow_pickle=False)
+    rays = torch.from_numpy(g2["rays4096"]).to(cuda)
+    gt = torch.from_numpy(g2["grad4096_gt"]).reshape(-1, 3).to(cuda)
+    cfg.task_arg.perturb = 0
+    cfg.task_arg.mlp_dtype = dtype
+    torch.manual_seed(0)
+    net = Network()
+    net.load_state_dict(_trained(), strict=True)
+    net = net.to(cuda)
+    trainer = make_trainer(cfg, net)
+    opt = make_optimizer(cfg, net)
+    batch = {"rays": rays[None], "rgbs": gt[None], "near": ops.device_scalar(2.0, cuda),
+             "far": ops.device_scalar(6.0, cuda)}
+    saved = (dict(ops.BWD_CHUNK), ops.DW_STREAM)
+    code = ops.pack_code(ops.dtype_code(dtype), 1)
+    grads = {}
+    try:
+        for name, chunk, stream in (("one", None, False), ("stream", None, True), ("chunk", 262144, False),
+                                    ("chunk+stream", 262144, True)):
+            ops.BWD_CHUNK = {code: chunk} if chunk else {}
+            ops.DW_STREAM = stream
+            trainer.forward_backward(dict(batch), opt)
+            torch.cuda.synchronize()
+            grads[name] = opt.flat_grad.clone()
+    finally:
+        ops.BWD_CHUNK, ops.DW_STREAM = saved
+        cfg.task_arg.mlp_dtype = "fp32"
+    assert torch.equal(grads["one"], grads["stream"])
+    assert torch.equal(grads["chunk"], grads["chunk+stream"])
+    for off, n in opt._ranges:  # per tensor of the flat gradient
+        a, b = grads["one"][off:off + n], grads["chunk"][off:off + n]
+        assert float((a - b).abs().max()) <= 1e-5 * float(a.abs().max()) + 1e-12, (dtype, off, n)

@@ -34,6 +34,10 @@ def main():
                     help="comma-separated sample counts: time the backward (dX then dW) run per chunk of that many "
                          "samples, so dW reads each chunk's dZ soon after dX wrote it (Infinity Cache, 256 MiB), "
                          "against the one-launch backward")
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="with --chunks: the training step's backward (the M-sample fine net in chunks, then an "
+                         "N-sample coarse net) with every dW on a second stream, so that the next dX overlaps it; "
+                         "N = this value")
     args = ap.parse_args()
     if args.lib:
         _lib.LIB_PATH = os.path.abspath(args.lib)
@@ -80,6 +84,8 @@ def main():
     out = {"M": M, "dtype": args.dtype}
     if args.chunks:
         kern["fwd_train"]()  # (act and masks of a real forward)
+        if args.overlap:
+            return overlapped_backward(args, L, dt, M, pb, d_raw, masks, act, dz, grad)
         return chunked_backward(args, L, dt, M, pb, d_raw, masks, act, dz, grad, s)
     for name, fn in kern.items():
         fn()
@@ -140,6 +146,70 @@ def chunked_backward(args, L, dt, M, pb, d_raw, masks, act, dz, grad, s):
         out["ms"][str(C)] = round(times[len(times) // 2], 4)
     g0 = grads[M]
     out["max_rel_diff_vs_one_launch"] = {str(C): float((grads[C] - g0).abs().max() / g0.abs().max()) for C in sizes[1:]}
+    print(json.dumps(out), flush=True)
+
+
+def overlapped_backward(args, L, dt, M, pb, d_raw, masks, act, dz, grad):
+    """The step's two MLP backwards (fine: M samples in chunks of C; then coarse: N samples, its
+    own buffers) run sequentially on one stream, against the same launches with every dW on a
+    second stream (event-ordered after its dX), so the next dX -- the fine net's next chunk, or
+    the coarse net's -- runs while the previous dW streams its dZ.  Prints median ms of each
+    form and whether the two gradients are bit-equal (they must be: the same launches)."""
+    dev = act.device
+    N = args.overlap
+    z_blk, a_blk = L.nerf_mlp_dz_bytes(dt, 256) // 8, L.nerf_mlp_act_bytes(dt, 256) // 8
+    m_blk = L.nerf_mlp_mask_bytes(256) // 8
+    main, side = torch.cuda.current_stream(), torch.cuda.Stream()
+    dz2 = torch.empty(L.nerf_mlp_dz_bytes(dt, N), dtype=torch.uint8, device=dev)
+    grad2 = torch.zeros_like(grad)
+    ws = [torch.empty(L.nerf_mlp_dw_workspace_bytes(dt, M), dtype=torch.uint8, device=dev) for _ in range(2)]
+    out = {"M": M, "N": N, "dtype": args.dtype, "ms": {}}
+    grads = {}
+
+    def job(C):  # (samples, dX args, dW args) per launch pair, in step order
+        jobs = []
+        for s0 in range(0, M, C):
+            m, b0 = min(C, M - s0), s0 // 32
+            jobs.append((m, d_raw.data_ptr() + s0 * 16, masks.data_ptr() + b0 * m_blk, dz.data_ptr() + b0 * z_blk,
+                         act.data_ptr() + b0 * a_blk, grad))
+        jobs.append((N, d_raw.data_ptr(), masks.data_ptr(), dz2.data_ptr(), act.data_ptr(), grad2))
+        return jobs
+
+    def run(C, overlap):
+        for i, (m, draw, msk, dzp, actp, g) in enumerate(job(C)):
+            check(L.nerf_mlp_bwd_dx(ptr(pb), dt, draw, m, msk, dzp, main.cuda_stream), "dx")
+            if overlap:
+                e = torch.cuda.Event()
+                e.record(main)
+                side.wait_event(e)
+                check(L.nerf_mlp_bwd_dw_ws(dt, m, actp, dzp, ptr(g), ptr(ws[1]), side.cuda_stream), "dw")
+            else:
+                check(L.nerf_mlp_bwd_dw_ws(dt, m, actp, dzp, ptr(g), ptr(ws[0]), main.cuda_stream), "dw")
+        if overlap:
+            e = torch.cuda.Event()
+            e.record(side)
+            main.wait_event(e)
+    for C in [int(c) for c in args.chunks.split(",")]:
+        for overlap in (False, True):
+            key = f"{C}_{'overlap' if overlap else 'seq'}"
+            grad.zero_()
+            grad2.zero_()
+            run(C, overlap)
+            torch.cuda.synchronize()
+            grads[key] = (grad.clone(), grad2.clone())
+            times = []
+            for _ in range(args.rounds):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(main)
+                for _ in range(args.reps):
+                    run(C, overlap)
+                b.record(main)
+                torch.cuda.synchronize()
+                times.append(a.elapsed_time(b) / args.reps)
+            times.sort()
+            out["ms"][key] = round(times[len(times) // 2], 4)
+        g_s, g_o = grads[f"{C}_seq"], grads[f"{C}_overlap"]
+        out[f"{C}_bit_equal"] = bool(torch.equal(g_s[0], g_o[0]) and torch.equal(g_s[1], g_o[1]))
     print(json.dumps(out), flush=True)
 
 

@@ -48,7 +48,7 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in d.items()}, {k: len(v) for k, v in d.items()}
 
 
-def main(fetch_csv, write_csv, dtype):
+def main(fetch_csv, write_csv, dtype, mlp_samples=524288):
     f, nf = per_kernel(fetch_csv, "FETCH_SIZE")
     w, _ = per_kernel(write_csv, "WRITE_SIZE")
     out = {}
@@ -56,9 +56,12 @@ def main(fetch_csv, write_csv, dtype):
         rd = 2.0 * f.get(k, 0.0)
         out[k] = {"launches": nf.get(k, 0), "read_bytes": rd, "write_bytes": w.get(k, 0.0),
                   "traffic_bytes": rd + w.get(k, 0.0)}
-    json.dump({"dtype": dtype, "unit": "bytes per launch", "kernels": out}, sys.stdout, indent=1)
+    # the MLP launches' mean samples: 524,288 when each net's backward is one launch (coarse
+    # 262,144 + fine 786,432); bench.py scales the MLP bytes to its own launches by it
+    json.dump({"dtype": dtype, "unit": "bytes per launch", "mlp_samples_per_launch": mlp_samples, "kernels": out},
+              sys.stdout, indent=1)
     print()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3])
+    main(sys.argv[1], sys.argv[2], sys.argv[3], *[int(x) for x in sys.argv[4:5]])
