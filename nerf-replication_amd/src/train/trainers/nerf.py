@@ -9,6 +9,7 @@ import torch.nn as nn
 
 from nerf_amd import ops
 
+from src.config import cfg
 from src.models.nerf.renderer.volume_renderer import Renderer
 
 
@@ -22,7 +23,7 @@ class NetworkWrapper(nn.Module):
     def forward(self, batch):
         ret = self.renderer.render(batch)
         gt = batch["rgbs"].reshape(-1, 3) if batch["rgbs"].dim() == 3 else batch["rgbs"]
-        if "rgb_map_f" in ret and ret["rgb_map_c"].is_cuda:
+        if "rgb_map_f" in ret and ret["rgb_map_c"].is_cuda and cfg.task_arg.get("fuse_mse", True):
             # both MSEs and their sum in one launch, the backward in one (ops.mse_pair)
             loss_c, loss_f, total = ops.mse_pair(ret["rgb_map_c"], ret["rgb_map_f"], gt)
             return ret, total, {"loss_c": loss_c, "loss_f": loss_f, "total_loss": total}

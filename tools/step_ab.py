@@ -9,6 +9,7 @@ Configurations (ops.BWD_CHUNK x ops.DW_STREAM):
   chunk    the backward in 262,144-sample chunks (dX, dW per chunk)
   stream   one launch each, dW on the dW stream (the next dX -- the coarse net's -- overlaps it)
   chunk+stream
+  unfused  one, with the round-4 fused launches split again (composite + sample_pdf, the MSE pair)
 Prints one JSON line: median ms/step per configuration.
 """
 import argparse
@@ -46,6 +47,8 @@ def main():
     def setup(c):
         ops.BWD_CHUNK = {code: a.chunk} if "chunk" in c else {}
         ops.DW_STREAM = "stream" in c
+        # "unfused": coarse composite + sample_pdf as two launches, MSE(c) + MSE(f) through torch
+        cfg.task_arg.fuse_composite_pdf = cfg.task_arg.fuse_mse = "unfused" not in c
 
     times = {c: [] for c in configs}
     for r in range(a.rounds + 1):
