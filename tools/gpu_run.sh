@@ -14,6 +14,7 @@
 #   mlp=ARGS         tools/mlp_bench.py ARGS (comma-free; use + for spaces)
 #   march=DTYPE      tools/march_bench.py --dtype DTYPE
 #   ab=DTYPE         tools/step_ab.py --dtype DTYPE (whole-step A/B of the backward scheduling knobs)
+#   abe=DTYPE        tools/step_ab.py --dtype DTYPE --configs one,events (cost of the per-kernel timing events)
 #   abu=DTYPE        tools/step_ab.py --dtype DTYPE --configs one,unfused (the round-4 fused launches split again)
 #   traffic=DTYPE    PMC FETCH_SIZE / WRITE_SIZE passes of a short bench -> gpurun_out/traffic_DTYPE.json
 # Logs go to gpurun_out/<step>.log.
@@ -54,6 +55,7 @@ for step in "$@"; do
           run "trW_$dt" 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/tr_$dt/W -o p --output-format csv -- $B
           python3 tools/pmc_traffic.py gpurun_out/tr_$dt/F/p_counter_collection.csv gpurun_out/tr_$dt/W/p_counter_collection.csv $dt > gpurun_out/traffic_$dt.json || exit 1 ;;
     mlp=*) args=${step#mlp=}; nm=$((nm + 1)); run "mlp$nm" 600 python3 tools/mlp_bench.py ${args//+/ } ;;
+    abe=*) run "abe_${step#abe=}" 600 python3 -u tools/step_ab.py --dtype "${step#abe=}" --configs one,events --rounds 7 ;;
     abu=*) run "abu_${step#abu=}" 600 python3 -u tools/step_ab.py --dtype "${step#abu=}" --configs one,unfused --rounds 7 ;;
     ab=*) run "ab_${step#ab=}" 600 python3 -u tools/step_ab.py --dtype "${step#ab=}" ;;
     march=*) run "march_${step#march=}" 400 python3 tools/march_bench.py --dtype "${step#march=}" ;;

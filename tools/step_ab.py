@@ -10,6 +10,7 @@ Configurations (ops.BWD_CHUNK x ops.DW_STREAM):
   stream   one launch each, dW on the dW stream (the next dX -- the coarse net's -- overlaps it)
   chunk+stream
   unfused  one, with the round-4 fused launches split again (composite + sample_pdf, the MSE pair)
+  events   one, with bench.py's per-kernel HIP timing events recorded (ops.KERNEL_TIMES)
 Prints one JSON line: median ms/step per configuration.
 """
 import argparse
@@ -49,6 +50,9 @@ def main():
         ops.DW_STREAM = "stream" in c
         # "unfused": coarse composite + sample_pdf as two launches, MSE(c) + MSE(f) through torch
         cfg.task_arg.fuse_composite_pdf = cfg.task_arg.fuse_mse = "unfused" not in c
+        # "events": bench.py's per-launch HIP timing events (ops.kernel_timer) recorded around every kernel
+        ops.KERNEL_TIMES.reset()
+        ops.KERNEL_TIMES.enabled = "events" in c
 
     times = {c: [] for c in configs}
     for r in range(a.rounds + 1):
