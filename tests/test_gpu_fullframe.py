@@ -117,7 +117,7 @@ def test_config2_full_frame_render(g4, frame, renderer, dtype):
     _compare(out, g4, "render", RENDER_KEYS, dtype)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16x3f"])
 def test_config4_full_frame_march(g4, frame, renderer, dtype):
     """Config 4: the frame through render_accelerated on the reference's res-128 bake of the
     same weights; the MLP query count over all 640,000 rays against the reference's."""
