@@ -68,9 +68,9 @@ def _batch(rays, rgbs, dev):
             "far": ops.device_scalar(6.0, dev)}
 
 
-def _worker(rank, world, port, dtype, q):
+def _worker(rank, world, port, dtype, q, dw_stream=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), NERF_AMD_NO_ARGV="1")
+                      LOCAL_RANK=str(rank), NERF_AMD_NO_ARGV="1", NERF_DW_STREAM="1" if dw_stream else "0")
     import sys
     sys.path[:0] = [ROOT, os.path.join(ROOT, "nerf-replication_amd")]
     try:
@@ -116,12 +116,14 @@ def _worker(rank, world, port, dtype, q):
         q.put((rank, False, None, None, None, False, False, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_two_rank_dp_step_matches_single_process(dtype):
+@pytest.mark.parametrize("dtype,dw_stream", [("fp32", False), ("bf16", False), ("bf16", True)])
+def test_two_rank_dp_step_matches_single_process(dtype, dw_stream):
+    """dw_stream: the opt-in NERF_DW_STREAM=1 schedule (every dW on a second stream; a bucket's
+    all-reduce is enqueued behind it) reduces the same gradient bit for bit."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, dtype, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, dtype, q, dw_stream)) for r in range(2)]
     for p in procs:
         p.start()
     try:
