@@ -18,9 +18,9 @@ same run and reported as nested, labelled lines: ``bf16x3_line`` (split-bf16 ope
 bf16 MFMAs per product, ~1e-5 relative per dot product; priced against 1/3 of the bf16 peak),
 ``bf16x3f_line`` (the bf16x3 forward -- its rgb/depth are bf16x3's -- with the bf16 backward)
 and ``bf16_line`` (north_star: rgb/depth within 2e-3).
-``vs_baseline`` divides by the reference's per-step op graph run eagerly by PyTorch-ROCm on
-the same GPU at the same MLP dtype and perturb (``baseline``); ``cpu_baseline`` is the same
-graph on the host cores (config 1).
+``vs_baseline`` of every line divides by ONE number: the reference's per-step fp32 op graph run
+eagerly by PyTorch-ROCm on the same GPU with perturb 1 (``baseline``: median of 21 steps, measured
+once per run after the tiers); ``cpu_baseline`` is the same graph on the host cores (config 1).
 """
 import argparse
 import json
@@ -647,15 +647,9 @@ def main():
             log(f"{dtype}: render {render_s:.3f} s/frame")
             grid = grid_times(cfg, net, ds, device)
             log(f"{dtype}: grid {grid}")
-        eager = None
-        if rank == 0 and world == 1 and not args.no_eager_baseline:
-            # bf16x3 stands in for fp32 arithmetic: its baseline is the reference's fp32 eager step
-            eager = eager_gpu_baseline(device, args.rays, "fp32" if dtype in ("bf16x3", "bf16x3f") else dtype)
-            log(f"{dtype}: eager PyTorch-ROCm {eager['value']} rays/s")
         lines[dtype] = {
             "value": round(value, 1), "ms_per_step": round(ms_step, 3), "dtype": dtype,
-            "vs_baseline": None if eager is None else round(value / world / eager["value"], 2),
-            "baseline": eager, "roofline": roofline, "kernels": kt,
+            "vs_baseline": None, "baseline": None, "roofline": roofline, "kernels": kt,
             "stream_kernels": {"train_step": train_stream, "render_800x800": render_stream},
             "render_s_per_frame": None if render_s is None else round(render_s, 4),
             "render_parallelism": f"tile-split over {world} GPU(s)", "occupancy_grid": grid,
@@ -663,15 +657,20 @@ def main():
         }
         del net, ds
         torch.cuda.empty_cache()
-    # the bf16 line is compared with the FASTER eager configuration: eager bf16 (autocast) is
-    # host-bound on this stack (each bf16 aten::mm in backward costs ~0.55 ms of host time,
-    # tools/eager_probe.py), so the reference's own fp32 eager step is the stronger baseline
-    if "bf16" in lines and "fp32" in lines:
-        eb, ef = lines["bf16"]["baseline"], lines["fp32"]["baseline"]
-        if eb is not None and ef is not None and ef["value"] > eb["value"]:
-            lines["bf16"]["baseline"] = dict(ef, note="eager fp32 is faster than eager bf16 autocast "
-                                                      f"({eb['value']} rays/s, host-bound); the faster one is used")
-            lines["bf16"]["vs_baseline"] = round(lines["bf16"]["value"] / world / ef["value"], 2)
+    # ONE denominator for every tier: the reference's own fp32 step run eagerly by PyTorch-ROCm,
+    # measured once per run after all tiers (median of 21 steps, min / max reported).  Eager bf16
+    # (autocast) is slower on this stack (host-bound: each bf16 aten::mm in backward costs ~0.55 ms
+    # of host time, tools/eager_probe.py), so the fp32 step is the stronger baseline for the bf16
+    # tier too; its autocast time is kept beside it for reference.
+    if rank == 0 and world == 1 and not args.no_eager_baseline:
+        eager = eager_gpu_baseline(device, args.rays, "fp32", reps=21)
+        log(f"eager PyTorch-ROCm fp32 {eager['value']} rays/s ({eager['ms_per_step_min_max']} ms min/max)")
+        for d in lines:
+            lines[d]["baseline"] = eager
+            lines[d]["vs_baseline"] = round(lines[d]["value"] / world / eager["value"], 2)
+        if "bf16" in lines:
+            eb = eager_gpu_baseline(device, args.rays, "bf16", reps=5)
+            lines["bf16"]["eager_bf16_autocast"] = {k: eb[k] for k in ("value", "ms_per_step", "ms_per_step_min_max")}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_rays)

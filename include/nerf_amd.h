@@ -30,6 +30,7 @@ extern "C" {
 #define NERF_DTYPE_F32 0
 #define NERF_DTYPE_BF16 1
 #define NERF_DTYPE_BF16X3 2 /* fp32 operands split into bf16 hi + lo: three bf16 MFMAs per product */
+#define NERF_DTYPE_BF16X3F 3 /* the bf16x3 forward (outputs bit-identical to bf16x3) + the bf16 backward */
 
 #define NERF_MLP_STORE 1   /* keep activations + ReLU masks for backward */
 #define NERF_MLP_DENSITY 2 /* sigma only (grid bake) */
@@ -93,7 +94,9 @@ int nerf_composite_pdf(const float* raw, const float* z, const float* dirs, int 
 
 /* ---- (a10) loss: MSE(rgb_map_c, gt) + MSE(rgb_map_f, gt) (src/train/trainers/nerf.py:21-29) -----
  * n = 3 R values.  fwd: out[3] = (loss_c, loss_f, loss_c + loss_f), one workgroup, fp64 sums in a
- * fixed order; f nullable.  bwd: gc = (2/n) (c - gt) (g_lc + g_total), gf = (2/n) (f - gt) (g_lf +
+ * fixed order (run-to-run identical); f nullable.  The losses are the correctly rounded means, so
+ * they can differ in the last bits from nn.MSELoss's fp32 CPU reduction: they are logged only --
+ * the backward needs no forward value, and its gradients equal torch's bit for bit.  bwd: gc = (2/n) (c - gt) (g_lc + g_total), gf = (2/n) (f - gt) (g_lf +
  * g_total) with device-scalar output grads (null = 0), ATen's rounding order. */
 int nerf_mse2_fwd(const float* c, const float* f, const float* gt, int64_t n, float* out, hipStream_t stream);
 int nerf_mse2_bwd(const float* c, const float* f, const float* gt, int64_t n, const float* g_lc, const float* g_lf,
@@ -115,7 +118,9 @@ int nerf_mse2_bwd(const float* c, const float* f, const float* gt, int64_t n, co
  * 2 = bf16x3 (operands split into bf16 hi + lo, three bf16 MFMAs per product, fp32 accumulation),
  * 3 = bf16x3f: the bf16x3 forward (its outputs are bf16x3's, bit for bit) whose training stores are
  * the bf16 (hi) halves, and the bf16 backward (dX chain, dW).  Every function maps 3 to its part:
- * packed_bytes / pack dir 0 and fwd -> bf16x3, pack dir 1 / act / dz bytes / bwd -> bf16. */
+ * packed_bytes / pack dir 0 and fwd -> bf16x3, pack dir 1 / act / dz bytes / bwd -> bf16.
+ * Any other dtype: the size helpers return -1, every launching function -22 (nerf_last_error
+ * names the dtype). */
 int64_t nerf_mlp_net_params(void);
 int64_t nerf_mlp_param_offset(int i);
 int64_t nerf_mlp_packed_bytes(int dtype, int dir);

@@ -30,6 +30,17 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 
+// (NERF_DIAG_EPI: diagnostic timing builds only -- the bf16x3 finish without its ReLU, mask bits
+// and lo half, results meaningless -- to price the epilogue in the kernels' time)
+#ifndef NERF_DIAG_EPI
+#define NERF_DIAG_EPI 0
+#endif
+// mask bits of the bf16x3 training forward from the packed hi pair (v_pk_min_u16 + v_lshl_or_b32
+// per register pair) instead of per-value compares and selects
+#ifndef NERF_PACKED_MASK
+#define NERF_PACKED_MASK 1
+#endif
+
 // registers 2k, 2k+1 of an fp32 accumulator as one packed bf16 pair (v_cvt_pk_bf16_f32)
 __device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
@@ -207,7 +218,7 @@ struct PBF3 {
     const uint32_t hw = pack_bf16(x0, x1);
     const uint32_t lw = pack_bf16(x0 - __uint_as_float(hw << 16), x1 - __uint_as_float(hw & 0xffff0000u));
     put(t.hi[k >> 2], k & 3, hw);
-    put(t.lo[k >> 2], k & 3, lw);
+    put(t.lo[k >> 2], k & 3, NERF_DIAG_EPI ? 0u : lw);
   }
 };
 
@@ -215,9 +226,6 @@ struct PBF3 {
 // (rho >> 1) + 16 (rho & 1) of a dword (bf16 pair k = registers 2k, 2k+1 -> bits k, 16 + k),
 // and two tiles n, n + 1 share one dword, the odd one shifted up by 8.
 __host__ __device__ constexpr int mask_bit(int rho) { return (rho >> 1) + 16 * (rho & 1); }
-#ifndef NERF_MASK_FROM_PACKED
-#define NERF_MASK_FROM_PACKED 0
-#endif
 
 typedef __attribute__((ext_vector_type(2))) short i16x2;
 typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
@@ -227,8 +235,12 @@ __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t d) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2, d), (i16x2){0, 0}));
 }
 // 1 in each half that is non-zero (v_pk_min_u16 with 1)
+// (asm: written with __builtin_elementwise_min, hipcc expands it into ~8 compares and selects
+// per pair once it knows the halves come from a ReLU'd conversion)
 __device__ __forceinline__ uint32_t nonzero_bf16x2(uint32_t d) {
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, d), (u16x2){1, 1}));
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(d), "s"(0x00010001u));
+  return r;
 }
 
 template <class P> __host__ __device__ constexpr int samples_per_block() { return P::WAVES * 32; }
@@ -369,11 +381,10 @@ __device__ __forceinline__ void sfor(F&& f) {
 
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 
-#ifndef NERF_NSLOT
-#define NERF_NSLOT 2
-#endif
-constexpr int NSLOT = NERF_NSLOT;                 // ring slots; DMA runs NSLOT - 1 groups ahead
-constexpr int SLOT_CAP = NSLOT == 2 ? 72 : 48;    // KiB (1 KiB chunks) per slot: <= 144 KiB of 160 KiB LDS
+// (a 3-slot ring of 48 KiB slots, DMA two groups ahead, measured slower everywhere in round 4:
+// profiles/r4/pipeline_experiments.json)
+constexpr int NSLOT = 2;       // ring slots; the DMA runs one group ahead
+constexpr int SLOT_CAP = 72;   // KiB (1 KiB chunks) per slot: 144 KiB of the 160 KiB LDS
 constexpr int PF = NSLOT - 1;
 constexpr int GROUP_MAX = 8;   // units per group
 #ifndef NERF_GROUP_ACROSS
@@ -446,25 +457,15 @@ __device__ __forceinline__ lds_cu4* lds_ptr(uint32_t byte_addr) {
 // input tile t, chunk c), in execution order.  A group's body is straight-line code over
 // it with the A operand (weights, LDS) prefetched PD steps ahead across unit boundaries
 // -- hipcc on its own keeps one ds_read in flight and waits lgkmcnt(0) before every MFMA.
-//
-// LDS-DMA batching: 1 = one global_load_lds (1 KiB) per M0 setting; 4 = a wave copies blocks of
-// 4 consecutive chunks with one M0 and the instruction offsets 0 / 1 / 2 / 3 KiB (applied to the
-// global and the LDS address alike), 5 instructions per 4 KiB instead of ~28
-#ifndef NERF_DMA_BATCH
-#define NERF_DMA_BATCH 1
-#endif
-constexpr int DMA_BATCH = NERF_DMA_BATCH;
-static_assert(DMA_BATCH == 1 || DMA_BATCH == 4, "NERF_DMA_BATCH must be 1 or 4");
-// DMA units (of DMA_BATCH wave-instructions) per wave for group g (fetch_group)
+
+// DMA wave-instructions (1 KiB global_load_lds each) per wave for group g (fetch_group)
 template <class P, int DIR, bool DENSITY>
 __host__ __device__ constexpr int group_dma_units(int g) {
-  const int nb = (GroupTable<DIR, DENSITY, P::CH>::t.g[g].nch + DMA_BATCH - 1) / DMA_BATCH;
-  return (nb + P::WAVES - 1) / P::WAVES;
+  return (GroupTable<DIR, DENSITY, P::CH>::t.g[g].nch + P::WAVES - 1) / P::WAVES;
 }
-// DMA wave-instructions per wave for group g
 template <class P, int DIR, bool DENSITY>
 __host__ __device__ constexpr int group_dma(int g) {
-  return group_dma_units<P, DIR, DENSITY>(g) * DMA_BATCH;
+  return group_dma_units<P, DIR, DENSITY>(g);
 }
 // vmcnt of the hand-off at the end of group g (group g + 1's DMA must have landed): the
 // wave's vector-memory ops younger than that DMA = the DMAs of groups g + 2 .. g + PF and
@@ -521,22 +522,17 @@ template <class P> __host__ __device__ constexpr int prefetch_depth() {
 }
 constexpr int FINISH_DELAY = NERF_FINISH_DELAY;
 
-// W: the wave object; it provides in_tile<u, t>(), prefetch<u>() (issue unit u's side
-// reads one unit ahead), init<u>(acc) (initial accumulator) and finish_part<u, p>(acc)
-#ifndef NERF_CROSS_GROUP_FINISH
-#define NERF_CROSS_GROUP_FINISH 1
-#endif
-// bf16x3 training forward: a finished accumulator carried over the barrier (plus the
-// hi / lo split of the finish) takes it past 512 VGPRs (139 spilled); finished in-group it
-// needs 438 and none
-#ifndef NERF_CROSS_GROUP_FINISH_BF3_FWD
-#define NERF_CROSS_GROUP_FINISH_BF3_FWD 0
+// Cross-group finish: the last unit of a group is finished after the barrier.  Not in the
+// bf16x3 forward: a finished accumulator carried over the barrier (plus the hi / lo split of
+// the finish) takes it past 512 VGPRs (139 spilled); finished in-group it needs none.
+#ifndef NERF_CROSS_FINISH_BF3_FWD
+#define NERF_CROSS_FINISH_BF3_FWD 0
 #endif
 template <class P, int DIR> __host__ __device__ constexpr bool cross_finish() {
-  return P::KIND == K_BF16X3 && DIR == 0 ? NERF_CROSS_GROUP_FINISH_BF3_FWD : NERF_CROSS_GROUP_FINISH;
+  return NERF_CROSS_FINISH_BF3_FWD || !(P::KIND == K_BF16X3 && DIR == 0);
 }
 // the unit finished inside group g: (first, last] = units whose finish is issued in g.
-// With CROSS_GROUP_FINISH the last unit of a group is finished FINISH_DELAY steps into the
+// With cross_finish() the last unit of a group is finished FINISH_DELAY steps into the
 // next group (after the barrier), so no group ends in a VALU burst that every wave of the
 // workgroup runs at once; its stores then count against the next group's hand-off.
 template <int DIR, bool DENSITY, int CH, bool CROSS>
@@ -680,20 +676,9 @@ __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
   });
 }
 
-// four consecutive 1 KiB chunks with one M0 (NERF_DMA_BATCH 4)
-__device__ __forceinline__ void glds16x4_asm(const void* gsrc, uint32_t lds_wave_base) {
-  if constexpr (NERF_DIAG_NO_DMA) return;
-  uint32_t saved;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-               "global_load_lds_dwordx4 %1, off\n\tglobal_load_lds_dwordx4 %1, off offset:1024\n\t"
-               "global_load_lds_dwordx4 %1, off offset:2048\n\tglobal_load_lds_dwordx4 %1, off offset:3072\n\t"
-               "s_mov_b32 m0, %0"
-               : "=&s"(saved) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_wave_base)) : "memory");
-}
-
-// DMA unit i of a wave for a group of NCH chunks starting at chunk C0 into slot `slot_base`:
-// every wave issues exactly group_dma_units units (the last chunk / block is re-copied by the
-// surplus waves -- identical bytes), so the count a later wait needs is a compile-time constant
+// DMA piece i of a wave for a group of NCH chunks starting at chunk C0 into slot `slot_base`:
+// every wave issues exactly group_dma_units pieces (the last chunk is re-copied by the surplus
+// waves -- identical bytes), so the count a later wait needs is a compile-time constant
 template <class P, int C0, int NCH, int I, bool LAUNDER = false>
 __device__ __forceinline__ void fetch_piece(const uint4* gsrc, uint32_t slot_base, int wave, int lane) {
   if constexpr (LAUNDER) {  // (persistent forward: the chunk indices are recomputed per group, not
@@ -701,21 +686,56 @@ __device__ __forceinline__ void fetch_piece(const uint4* gsrc, uint32_t slot_bas
     settle(w);
     wave = (int)w;
   }
-  if constexpr (DMA_BATCH == 1) {
-    const int k = cmin(wave + P::WAVES * I, NCH - 1);
-    glds16_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
+  const int k = cmin(wave + P::WAVES * I, NCH - 1);
+  glds16_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
+}
+
+// Lean form of the same piece (NERF_DMA_LEAN): 3 instructions instead of 7.  Wave w's piece I is
+// chunk w + WAVES I, so with the per-lane VGPR vlane = 16 lane + 1024 w and the wave-uniform
+// swave = LDS base + 1024 w held for the whole kernel, the piece's global offset and LDS address
+// are those plus compile-time constants: `s_add_u32 m0` (the LDS destination), `v_add_u32` (the
+// per-lane offset, SADDR form on the packed-weight base; it is also the wait state the m0 write
+// needs before the DMA) and the DMA.  M0 is not saved: no compiler code of these kernels touches
+// it (tools/asm_check.py checks the emitted code).  s_add_u32 writes SCC: declared clobbered (without
+// it hipcc kept a comparison in SCC across the statement and the last group's surplus-wave
+// selection went wrong -- the rgb bias chunk was never copied).  A surplus wave of the last piece
+// (w + WAVES I > NCH - 1) re-copies its previous piece instead: the same bytes to the same place.
+#ifndef NERF_DMA_LEAN
+#define NERF_DMA_LEAN 1
+#endif
+struct DmaLean {
+  const void* gbase;  // packed weights (kernel argument: SGPR pair)
+  uint32_t vlane;     // 16 lane + 1024 wave
+  uint32_t swave;     // LDS byte address of the ring + 1024 wave (wave-uniform)
+  uint32_t wave_u;    // wave (wave-uniform)
+};
+template <class P, int C0, int NCH, int SLOT_OFF, int I>
+__device__ __forceinline__ void fetch_piece_lean(const DmaLean& d) {
+  if constexpr (NERF_DIAG_NO_DMA) return;
+  constexpr int NU = (NCH + P::WAVES - 1) / P::WAVES;
+  constexpr uint32_t GOFF = (uint32_t)(C0 + P::WAVES * I) * 1024u, LOFF = (uint32_t)(SLOT_OFF + P::WAVES * I * 1024);
+  static_assert(NCH % P::WAVES == 0 || NU >= 2, "a one-piece group with surplus waves");
+  uint32_t tmp;
+  if constexpr (I + 1 < NU || NCH % P::WAVES == 0) {
+    asm volatile("s_add_u32 m0, %1, %3\n\tv_add_u32 %0, %4, %2\n\tglobal_load_lds_dwordx4 %0, %5"
+                 : "=&v"(tmp) : "s"(d.swave), "v"(d.vlane), "i"(LOFF), "i"(GOFF), "s"(d.gbase) : "memory", "scc");
   } else {
-    static_assert(NCH >= 4, "a DMA block needs 4 chunks");
-    constexpr int NB = (NCH + 3) / 4;
-    const int b = cmin(wave + P::WAVES * I, NB - 1);
-    const int k = cmin(4 * b, NCH - 4);  // (the last block overlaps its predecessor: same bytes)
-    glds16x4_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
+    const uint32_t adj = d.wave_u + P::WAVES * I > (uint32_t)(NCH - 1) ? (uint32_t)P::WAVES * 1024u : 0u;
+    asm volatile("s_add_u32 m0, %1, %3\n\tv_add_u32 %0, %4, %2\n\tglobal_load_lds_dwordx4 %0, %5"
+                 : "=&v"(tmp) : "s"(d.swave - adj), "v"(d.vlane), "i"(LOFF), "s"(GOFF - adj), "s"(d.gbase)
+                 : "memory", "scc");
   }
 }
-// issue the whole DMA of group G into slot `slot` (group_dma_units units per wave)
+template <class P, int C0, int NCH, int SLOT_OFF>
+__device__ __forceinline__ void fetch_group_lean(const DmaLean& d) {
+  constexpr int NU = (NCH + P::WAVES - 1) / P::WAVES;
+  sfor<NU>([&](auto ii) { fetch_piece_lean<P, C0, NCH, SLOT_OFF, decltype(ii)::value>(d); });
+}
+
+// issue the whole DMA of group G into slot `slot` (group_dma_units pieces per wave)
 template <class P, int C0, int NCH, bool LAUNDER = false>
 __device__ __forceinline__ void fetch_group(const uint4* gsrc, uint32_t slot_base, int wave, int lane) {
-  constexpr int NU = ((NCH + DMA_BATCH - 1) / DMA_BATCH + P::WAVES - 1) / P::WAVES;
+  constexpr int NU = (NCH + P::WAVES - 1) / P::WAVES;
   sfor<NU>([&](auto ii) { fetch_piece<P, C0, NCH, decltype(ii)::value, LAUNDER>(gsrc, slot_base, wave, lane); });
 }
 
@@ -813,44 +833,30 @@ __device__ __forceinline__ void pe_tile(typename P::Tile& t, int h, float x0, fl
   if constexpr (P::KIND == K_BF16X3) P::pack16(t, vals);
 }
 
-// fragment-native store of one finished tile (mlp_tables.h, "Training stores"): CH
-// lane-linear 16-byte stores per lane, each wave-instruction writes 1 KiB contiguous
-#ifndef NERF_BLOCK_MAJOR
-#define NERF_BLOCK_MAJOR 1
-#endif
 // KiB offset of chunk c of tile tau of 32-sample block b in a store of `ntiles` tiles.
 // Block-major: one block's tiles are contiguous (a dW job reads a few contiguous runs per
 // block instead of one 1-2 KiB piece from each of up to 18 distant tile planes).
 __host__ __device__ constexpr int64_t tile_kib(int64_t nblk, int ntiles, int tau, int64_t b, int c, int ch) {
-  return NERF_BLOCK_MAJOR ? ((b * ntiles + tau) * ch + c) : (((int64_t)tau * nblk + b) * ch + c);
+  return (b * ntiles + tau) * ch + c;
 }
 // KiB stride between consecutive blocks of one tile
 __host__ __device__ constexpr int64_t block_stride_kib(int ntiles, int ch) {
-  return NERF_BLOCK_MAJOR ? (int64_t)ntiles * ch : ch;
+  return (int64_t)ntiles * ch;
 }
 
 // fragment-native store of one finished tile (mlp_tables.h, "Training stores"): CH
 // lane-linear 16-byte stores per lane, each wave-instruction writes 1 KiB contiguous
 //
-// Cache policy of the training stores (activations, dZ, masks: written once, read once by a
-// later kernel, gigabytes per launch): 0 plain, 1 nt, 2 sc1.  Measured per launch at 524,288
-// samples (tools/mlp_bench.py --libs, interleaved): nt takes the training forward 5.22 -> 4.94
-// ms (fp32), 0.737 -> 0.667 (bf16), 2.38 -> 2.02 (bf16x3) and dX 4.49 -> 4.35 / 0.692 -> 0.626 /
-// 1.92 -> 1.78; sc1 (drops the line from L2) gains as much on fp32 and less on bf16.
-#ifndef NERF_STORE_POLICY
-#define NERF_STORE_POLICY 1
-#endif
+// The training stores (activations, dZ, masks: written once, read once by a later kernel,
+// gigabytes per launch) are nontemporal.  Measured per launch at 524,288 samples
+// (tools/mlp_bench.py --libs, interleaved): nt takes the training forward 5.22 -> 4.94 ms
+// (fp32), 0.737 -> 0.667 (bf16), 2.38 -> 2.02 (bf16x3) and dX 4.49 -> 4.35 / 0.692 -> 0.626 /
+// 1.92 -> 1.78 against plain stores; sc1 gained as much on fp32 and less on bf16.
 template <int OFF>
 __device__ __forceinline__ void store16(uint4* p, uint4 v) {
   if constexpr (NERF_DIAG_NO_STORE) return;
   const u32x4 w = {v.x, v.y, v.z, v.w};
-  if constexpr (NERF_STORE_POLICY == 1) {
-    __builtin_nontemporal_store(w, (u32x4*)p + OFF / 16);
-  } else if constexpr (NERF_STORE_POLICY == 2) {
-    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc1" ::"v"(p), "v"(w), "i"(OFF));
-  } else {
-    p[OFF / 16] = v;
-  }
+  __builtin_nontemporal_store(w, (u32x4*)p + OFF / 16);
 }
 // SCH: chunks stored per tile (P::CH; 2 for a bf16x3 tile stored as its bf16 hi half, the
 // bf16 tile-block layout)
@@ -925,6 +931,7 @@ struct FwdWave {
   lds_cu4* wb;      // current group's slot + 16 h (bias reads)
   uint4 bias[4];
   f32x16 pend;      // finished accumulator awaiting its deferred finish (group_body)
+  DmaLean dl;
 
   __device__ __forceinline__ FwdWave(const FwdArgs& args, const uint4* smem, int64_t blk, int tid)
       : a(args), lds(smem) {
@@ -935,16 +942,21 @@ struct FwdWave {
     h = lane >> 5;
     wblock = blk * P::WAVES + wave;
     m = wblock * 32 + (lane & 31);
+    dl = DmaLean{a.wpack, (uint32_t)(lane * 16 + wave * 1024),
+                 (uint32_t)__builtin_amdgcn_readfirstlane(lds_base + (uint32_t)wave * 1024u),
+                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)wave)};
   }
 
   template <int g> __device__ __forceinline__ void fetch() {
     constexpr Group G = GT::t.g[g];
-    fetch_group<P, G.c0, G.nch, PERSIST>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
+    if constexpr (NERF_DMA_LEAN) fetch_group_lean<P, G.c0, G.nch, (g % NSLOT) * SLOT_CAP * 1024>(dl);
+    else fetch_group<P, G.c0, G.nch, PERSIST>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
   }
   template <int g, int i> __device__ __forceinline__ void fetch_piece() {
     constexpr Group G = GT::t.g[g];
-    nerf::mlp::fetch_piece<P, G.c0, G.nch, i, PERSIST>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024),
-                                                       wave, lane);
+    if constexpr (NERF_DMA_LEAN) fetch_piece_lean<P, G.c0, G.nch, (g % NSLOT) * SLOT_CAP * 1024, i>(dl);
+    else nerf::mlp::fetch_piece<P, G.c0, G.nch, i, PERSIST>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024),
+                                                            wave, lane);
   }
 
   // input tile t of layer L (mlp_tables.h: Ha/Hb ping-pong, PE tiles X / D)
@@ -989,16 +1001,26 @@ struct FwdWave {
         constexpr int k = K0 + decltype(kk)::value;
         const float a0 = acc[2 * k], a1 = acc[2 * k + 1];
         if constexpr (P::KIND == K_BF16) {
-          // bf16: pack the pair first, then ReLU on the packed pair (one VALU for both)
-          if constexpr (STORE) {
+          // bf16: pack the pair first, then ReLU on the packed pair (one VALU for both); the mask
+          // bits k / 16 + k from the packed result (as the bf16x3 path, NERF_PACKED_MASK)
+          const uint32_t d = relu_bf16x2(pack_bf16(a0, a1));
+          if constexpr (STORE && NERF_PACKED_MASK) {
+            bits |= nonzero_bf16x2(d) << k;
+          } else if constexpr (STORE) {
             bits |= (a0 > 0.f ? 1u : 0u) << mask_bit(2 * k);
             bits |= (a1 > 0.f ? 1u : 0u) << mask_bit(2 * k + 1);
           }
-          P::set_dword(out, k, relu_bf16x2(pack_bf16(a0, a1)));
+          P::set_dword(out, k, d);
+        } else if constexpr (P::KIND == K_BF16X3 && NERF_DIAG_EPI) {
+          P::set_pair(out, k, a0, a1);
         } else {
           // ReLU as an integer max on the float bits (negative floats are negative ints)
           const int y0 = max(__float_as_int(a0), 0), y1 = max(__float_as_int(a1), 0);
-          if constexpr (STORE) {
+          if constexpr (STORE && P::KIND == K_BF16X3 && NERF_PACKED_MASK) {
+            // bit k / 16 + k = the pair's hi halves non-zero: the same bits as y > 0, since RNE keeps
+            // every positive fp32 above 2^-134 non-zero in bf16 (pre-activations that small do not occur)
+            bits |= nonzero_bf16x2(pack_bf16(__int_as_float(y0), __int_as_float(y1))) << k;
+          } else if constexpr (STORE) {
             bits |= min((uint32_t)y0, 1u) << mask_bit(2 * k);
             bits |= min((uint32_t)y1, 1u) << mask_bit(2 * k + 1);
           }
@@ -1129,15 +1151,6 @@ struct FwdWave {
   }
 };
 
-#ifndef NERF_SETPRIO_YOUNG
-#define NERF_SETPRIO_YOUNG 0
-#endif
-// MI355X_MICROARCH.md "Two waves per SIMD" item 4: waves 4-7 lose VALU arbitration; one
-// static s_setprio 1 for them (wave-uniform condition via readfirstlane)
-__device__ __forceinline__ void young_priority() {
-  if (NERF_SETPRIO_YOUNG && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-}
-
 // PERSIST (inference only): the sample count is read on the device (a.M_dev, e.g. the grid
 // march's gather count: no host round trip sizes the launch) and a grid of one wave of
 // workgroups loops over the sample blocks; the barrier at the end of each block keeps the next
@@ -1145,7 +1158,6 @@ __device__ __forceinline__ void young_priority() {
 template <class P, bool STORE, bool DENSITY, bool PERSIST, bool HALF = false>
 __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
-  young_priority();
   if constexpr (!PERSIST) {
     FwdWave<P, STORE, DENSITY, false, HALF> w(a, smem_u4, blockIdx.x, threadIdx.x);
     w.run();
@@ -1195,6 +1207,7 @@ struct DxWave {
   Tile G, DA, Ha[8], Hb[8];
   uint4 mk[MASK_GROUPS];
   f32x16 pend;      // finished accumulator awaiting its deferred finish (group_body)
+  DmaLean dl;
 
   __device__ __forceinline__ DxWave(const DxArgs& args, const uint4* smem) : a(args), lds(smem) {
     gw = (const uint4*)a.wpack_t;
@@ -1204,15 +1217,21 @@ struct DxWave {
     h = lane >> 5;
     wblock = (int64_t)blockIdx.x * P::WAVES + wave;
     m = wblock * 32 + (lane & 31);
+    dl = DmaLean{a.wpack_t, (uint32_t)(lane * 16 + wave * 1024),
+                 (uint32_t)__builtin_amdgcn_readfirstlane(lds_base + (uint32_t)wave * 1024u),
+                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)wave)};
   }
 
   template <int g> __device__ __forceinline__ void fetch() {
     constexpr Group Gr = GT::t.g[g];
-    fetch_group<P, Gr.c0, Gr.nch>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
+    if constexpr (NERF_DMA_LEAN) fetch_group_lean<P, Gr.c0, Gr.nch, (g % NSLOT) * SLOT_CAP * 1024>(dl);
+    else fetch_group<P, Gr.c0, Gr.nch>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
   }
   template <int g, int i> __device__ __forceinline__ void fetch_piece() {
     constexpr Group Gr = GT::t.g[g];
-    nerf::mlp::fetch_piece<P, Gr.c0, Gr.nch, i>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave, lane);
+    if constexpr (NERF_DMA_LEAN) fetch_piece_lean<P, Gr.c0, Gr.nch, (g % NSLOT) * SLOT_CAP * 1024, i>(dl);
+    else nerf::mlp::fetch_piece<P, Gr.c0, Gr.nch, i>(gw, lds_base + (uint32_t)((g % NSLOT) * SLOT_CAP * 1024), wave,
+                                                     lane);
   }
   static __host__ __device__ constexpr int unit_stores(int) { return CH; }
 
@@ -1325,7 +1344,6 @@ struct DxWave {
 template <class P>
 __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
-  young_priority();
   DxWave<P> w(a, smem_u4);
   w.run();
 }
@@ -2053,11 +2071,18 @@ void mlp_fwd_train_half_impl(const FwdArgs& a, hipStream_t stream);
 #if defined(NERF_MLP_PREC) && NERF_MLP_PREC == 2 && (!defined(NERF_MLP_PART) || NERF_MLP_PART == 4)
 void mlp_fwd_train_half_impl(const FwdArgs& a, hipStream_t stream) { launch_fwd<PBF3, true, false, true>(a, stream); }
 #endif
+// the three inference forwards, one translation unit each (parts 1, 5, 6)
+template <class P>
+void mlp_fwd_plain_impl(const FwdArgs& a, hipStream_t stream) { launch_fwd<P, false, false>(a, stream); }
+template <class P>
+void mlp_fwd_density_impl(const FwdArgs& a, hipStream_t stream) { launch_fwd<P, false, true>(a, stream); }
+template <class P>
+void mlp_fwd_persist_impl(const FwdArgs& a, hipStream_t stream) { launch_fwd_persist<P>(a, stream); }
 template <class P>
 void mlp_fwd_infer_impl(const FwdArgs& a, bool density, hipStream_t stream) {
-  if (a.M_dev) launch_fwd_persist<P>(a, stream);
-  else if (density) launch_fwd<P, false, true>(a, stream);
-  else launch_fwd<P, false, false>(a, stream);
+  if (a.M_dev) mlp_fwd_persist_impl<P>(a, stream);
+  else if (density) mlp_fwd_density_impl<P>(a, stream);
+  else mlp_fwd_plain_impl<P>(a, stream);
 }
 template <class P>
 void mlp_dx_impl(const DxArgs& x, int64_t ldm, hipStream_t stream) {
@@ -2073,11 +2098,14 @@ void mlp_dw_impl(const DwArgs& w, dim3 grid, hipStream_t stream) {
 // of the large straight-line kernels
 #define NERF_MLP_I_PACK(EXT, P) EXT template void mlp_pack_impl<P>(const ParamPtrs&, int, char*, hipStream_t);
 #define NERF_MLP_I_FWDT(EXT, P) EXT template void mlp_fwd_train_impl<P>(const FwdArgs&, hipStream_t);
-#define NERF_MLP_I_FWDI(EXT, P) EXT template void mlp_fwd_infer_impl<P>(const FwdArgs&, bool, hipStream_t);
+#define NERF_MLP_I_FWDI(EXT, P) EXT template void mlp_fwd_plain_impl<P>(const FwdArgs&, hipStream_t);
+#define NERF_MLP_I_FWDD(EXT, P) EXT template void mlp_fwd_density_impl<P>(const FwdArgs&, hipStream_t);
+#define NERF_MLP_I_FWDP(EXT, P) EXT template void mlp_fwd_persist_impl<P>(const FwdArgs&, hipStream_t);
 #define NERF_MLP_I_DX(EXT, P) EXT template void mlp_dx_impl<P>(const DxArgs&, int64_t, hipStream_t);
 #define NERF_MLP_I_DW(EXT, P) EXT template void mlp_dw_impl<P>(const DwArgs&, dim3, hipStream_t);
 #define NERF_MLP_IMPLS(EXT, P) \
-  NERF_MLP_I_PACK(EXT, P) NERF_MLP_I_FWDT(EXT, P) NERF_MLP_I_FWDI(EXT, P) NERF_MLP_I_DX(EXT, P) NERF_MLP_I_DW(EXT, P)
+  NERF_MLP_I_PACK(EXT, P) NERF_MLP_I_FWDT(EXT, P) NERF_MLP_I_FWDI(EXT, P) NERF_MLP_I_FWDD(EXT, P) \
+  NERF_MLP_I_FWDP(EXT, P) NERF_MLP_I_DX(EXT, P) NERF_MLP_I_DW(EXT, P)
 #if !defined(NERF_MLP_PREC)
 NERF_MLP_IMPLS(extern, PF32)
 NERF_MLP_IMPLS(extern, PBF16)
@@ -2095,6 +2123,12 @@ NERF_MLP_I_FWDT(, NERF_PP)
 #endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 1
 NERF_MLP_I_FWDI(, NERF_PP)
+#endif
+#if !defined(NERF_MLP_PART) || NERF_MLP_PART == 5
+NERF_MLP_I_FWDD(, NERF_PP)
+#endif
+#if !defined(NERF_MLP_PART) || NERF_MLP_PART == 6
+NERF_MLP_I_FWDP(, NERF_PP)
 #endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 2
 NERF_MLP_I_DX(, NERF_PP)
@@ -2128,9 +2162,11 @@ int64_t nerf_mlp_packed_bytes(int dtype, int dir) {
 
 int64_t nerf_mlp_padded_samples(int64_t M) { return (M + M_ALIGN - 1) / M_ALIGN * M_ALIGN; }
 int64_t nerf_mlp_act_bytes(int dtype, int64_t M) {
+  if (dtype < 0 || dtype > 3 || M < 0) return -1;
   return (int64_t)A_ROWS * nerf_mlp_padded_samples(M) * (store_prec(dtype) == 1 ? 2 : 4);
 }
 int64_t nerf_mlp_dz_bytes(int dtype, int64_t M) {
+  if (dtype < 0 || dtype > 3 || M < 0) return -1;
   return (int64_t)Z_ROWS * nerf_mlp_padded_samples(M) * (store_prec(dtype) == 1 ? 2 : 4);
 }
 int64_t nerf_mlp_mask_bytes(int64_t M) { return nerf_mlp_padded_samples(M) / 32 * MASK_GROUPS * 64 * 16; }
@@ -2301,6 +2337,7 @@ static void dw_items(int dtype, int64_t nblk, int item_off[NDWJOB + 1], int job_
 #endif
 }
 int64_t nerf_mlp_dw_items(int dtype, int64_t M) {
+  if (dtype < 0 || dtype > 3 || M < 0) return -1;
   int off[NDWJOB + 1], job[NDWJOB];
   dw_items(bwd_prec(dtype), nerf_mlp_padded_samples(M) / 32, off, job);
   return off[NDWJOB];
@@ -2323,7 +2360,8 @@ int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64
 }
 
 int64_t nerf_mlp_dw_workspace_bytes(int dtype, int64_t M) {
-  return nerf_mlp_dw_items(dtype, M) * (int64_t)DW_PITEM * 4;
+  const int64_t items = nerf_mlp_dw_items(dtype, M);
+  return items < 0 ? -1 : items * (int64_t)DW_PITEM * 4;
 }
 
 // dW/db only: grad += dz . act^T (grad must be zeroed or hold a running sum).  workspace (nullable,

@@ -69,11 +69,30 @@ class Network(nn.Module):
         self.model = NeRF(**kw)
         self.model_fine = NeRF(**kw)
 
+    def mlp_dtype_for(self, model, fn):
+        """The MLP arithmetic of one forward.  The bf16x3 tiers (bf16x3, bf16x3f) evaluate the
+        COARSE net at fp32 when no autograd graph is recorded (render / evaluate / video):
+        render()'s importance samples are a deterministic function of the coarse weights at
+        perturb 0 (volume_renderer.py:82-134, u = linspace), and on the trained lego-class net a
+        split-bf16 coarse MLP (~1e-5 relative per dot product) moves a sample across a CDF bin
+        on a few rays of an 800x800 frame -- fine depth off by up to 3.7e-2 -- where an exact MLP
+        moves them by < 1.4e-4 (tools/fullframe_conditioning.py, profiles/r5/).  With the fp32
+        coarse pass every value of the frame holds the north_star's 2e-3.  The training forward
+        (autograd) keeps bf16x3: at perturb 1 the importance samples are random draws from the
+        CDF, which a 1e-5 relative perturbation leaves distributed the same.
+        task_arg.coarse_inference_dtype (default fp32) overrides the choice."""
+        dt = self.mlp_dtype
+        if model != "fine" and dt in ("bf16x3", "bf16x3f"):
+            recording = torch.is_grad_enabled() and any(p.requires_grad for p in fn.parameters())
+            if not recording:
+                dt = cfg.task_arg.get("coarse_inference_dtype", "fp32") or dt
+        return dt
+
     def forward(self, inputs, viewdirs, model=""):
         """inputs [R,S,3], viewdirs [R,3] -> raw [R,S,4] (network.py:171-192)."""
         fn = self.model_fine if model == "fine" else self.model
         R, S = inputs.shape[0], inputs.shape[1]
-        raw = fn(inputs.reshape(-1, 3), viewdirs, S, None, self.mlp_dtype)
+        raw = fn(inputs.reshape(-1, 3), viewdirs, S, None, self.mlp_dtype_for(model, fn))
         return raw.reshape(R, S, 4)
 
     def density(self, pts, model=""):

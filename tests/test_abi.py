@@ -76,3 +76,80 @@ def test_product_path_does_not_import_the_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", src, flags=re.M), os.path.join(dirpath, f)
+
+
+def test_bf16x3f_dtype_maps_to_its_parts(lib):
+    """NERF_DTYPE_BF16X3F (3): forward pack = bf16x3's, backward pack / stores = bf16's
+    (nerf_amd.h: "Every function maps 3 to its part")."""
+    text = open(HEADER).read()
+    codes = dict(re.findall(r"#define (NERF_DTYPE_\w+) (\d+)", text))
+    assert codes == {"NERF_DTYPE_F32": "0", "NERF_DTYPE_BF16": "1", "NERF_DTYPE_BF16X3": "2", "NERF_DTYPE_BF16X3F": "3"}
+    assert lib.nerf_mlp_packed_bytes(3, 0) == lib.nerf_mlp_packed_bytes(2, 0)
+    assert lib.nerf_mlp_packed_bytes(3, 1) == lib.nerf_mlp_packed_bytes(1, 1)
+    for M in (1, 4097, 786432):
+        assert lib.nerf_mlp_act_bytes(3, M) == lib.nerf_mlp_act_bytes(1, M) == lib.nerf_mlp_act_bytes(2, M) // 2
+        assert lib.nerf_mlp_dz_bytes(3, M) == lib.nerf_mlp_dz_bytes(1, M)
+
+
+@pytest.mark.parametrize("dtype", [-1, 4, 7])
+def test_bad_dtype_is_rejected_everywhere(lib, dtype):
+    """Every MLP entry point refuses a dtype outside 0..3 before touching any pointer (no GPU
+    needed: the argument checks run first)."""
+    import ctypes
+    from nerf_amd._lib import check
+    for helper in ("nerf_mlp_act_bytes", "nerf_mlp_dz_bytes"):
+        assert getattr(lib, helper)(dtype, 256) == -1, helper
+    assert lib.nerf_mlp_packed_bytes(dtype, 0) == -1 and lib.nerf_mlp_packed_bytes(dtype, 1) == -1
+    params = ctypes.cast((ctypes.c_void_p * 24)(*([None] * 24)), ctypes.c_void_p)
+    calls = {
+        "nerf_mlp_pack": lambda: lib.nerf_mlp_pack(params, dtype, None, None, None),
+        "nerf_mlp_fwd": lambda: lib.nerf_mlp_fwd(None, dtype, None, None, 1, None, 10, 0, None, None, None, None),
+        "nerf_mlp_fwd_count": lambda: lib.nerf_mlp_fwd_count(None, dtype, None, None, 1, None, None, 10, None, None),
+        "nerf_mlp_bwd_dx": lambda: lib.nerf_mlp_bwd_dx(None, dtype, None, 10, None, None, None),
+        "nerf_mlp_bwd_dw_ws": lambda: lib.nerf_mlp_bwd_dw_ws(dtype, 10, None, None, None, None, None),
+        "nerf_mlp_bwd": lambda: lib.nerf_mlp_bwd(None, dtype, None, 10, None, None, None, None, None),
+    }
+    for name, call in calls.items():
+        with pytest.raises(RuntimeError, match="dtype"):
+            check(call(), name)
+
+
+@pytest.mark.gpu
+def test_bf16x3f_through_the_c_abi(cuda, seeded_state):
+    """nerf_mlp_pack + nerf_mlp_fwd called through the C ABI (ctypes, no torch wrapper) with
+    NERF_DTYPE_BF16X3F: raw is bf16x3's bit for bit, the training stores are the bf16 (hi) halves
+    of bf16x3's (bf16 layout, half the bytes), the masks are bf16x3's; dtype 4 is refused."""
+    import ctypes
+    import torch
+    from nerf_amd import ops
+    from nerf_amd._lib import check, lib as L, ptr, stream_of
+    L = L()
+    M, spd = 4133, 7
+    g = torch.Generator().manual_seed(5)
+    pts = (torch.rand(M, 3, generator=g) * 2.6 - 1.3).to(cuda)
+    vd = torch.nn.functional.normalize(torch.randn(-(-M // spd), 3, generator=g), dim=-1).to(cuda)
+    params = [seeded_state[f"model.{n}"].to(cuda) for n in ops.NET_PARAM_NAMES]
+    arr = ctypes.cast((ctypes.c_void_p * 24)(*[p.data_ptr() for p in params]), ctypes.c_void_p)
+    s = stream_of(pts)
+    out = {}
+    for code in (2, 3):
+        fwd = torch.empty(L.nerf_mlp_packed_bytes(code, 0), dtype=torch.uint8, device=cuda)
+        bwd = torch.empty(L.nerf_mlp_packed_bytes(code, 1), dtype=torch.uint8, device=cuda)
+        check(L.nerf_mlp_pack(arr, code, ptr(fwd), ptr(bwd), s), "pack")
+        act = torch.zeros(L.nerf_mlp_act_bytes(code, M), dtype=torch.uint8, device=cuda)
+        masks = torch.zeros(L.nerf_mlp_mask_bytes(M), dtype=torch.uint8, device=cuda)
+        raw = torch.empty(M, 4, device=cuda)
+        check(L.nerf_mlp_fwd(ptr(fwd), code, ptr(pts), ptr(vd), spd, None, M, 1, ptr(raw), ptr(act), ptr(masks), s),
+              "fwd")
+        out[code] = (fwd, bwd, raw, act, masks)
+    torch.cuda.synchronize()
+    assert torch.equal(out[2][0], out[3][0])  # forward pack: bf16x3's
+    assert out[3][1].numel() == L.nerf_mlp_packed_bytes(1, 1)
+    assert torch.equal(out[2][2], out[3][2])  # raw bit for bit
+    assert torch.equal(out[2][4], out[3][4])  # ReLU masks
+    # bf16x3 tile-block = hi (2 KiB) then lo (2 KiB); bf16x3f keeps the hi 2 KiB of each
+    hi = out[2][3].view(-1, 4096)[:, :2048].reshape(-1)
+    assert torch.equal(hi, out[3][3])
+    raw = torch.empty(M, 4, device=cuda)
+    with pytest.raises(RuntimeError, match="dtype"):
+        check(L.nerf_mlp_fwd(ptr(out[3][0]), 4, ptr(pts), ptr(vd), spd, None, M, 0, ptr(raw), None, None, s), "fwd")

@@ -11,15 +11,19 @@ evaluator's uint8 frame and the march's query count over the frame.
 Here the whole 640,000-ray frame goes through the drop-in Renderer -- render() in its
 262,144-ray render chunks (M = 50.3 M fine samples per MLP launch), render_accelerated() in one
 march -- and is compared with NO exclusions:
-  * the 4,096 rays, every key: within 1e-4 (fp32, measured 4.6e-5); bf16x3 / bf16x3f (split-bf16
-    products, ~1e-5 relative each): >= 95 % within 1e-4 and >= 99.9 % within the north_star's
-    2e-3, every value within 5e-3 (measured: one fine depth of the 4,096 at 3.4e-3, a ray whose
-    importance samples move bins);
-  * every row sum within 800 x the per-value tolerance (so every row of the frame is covered,
-    not only the sampled rays);
-  * the uint8 frame (clip(rgb) x 255, truncated): fp32 every pixel within one level, >= 99.9 %
-    identical (measured 99.999 %); bf16x3 / bf16x3f >= 99.95 % identical and within 8 levels
-    (measured 99.981 %, max 6: a few pixels, outside the 4,096, where the fine integral flips);
+  * the 4,096 rays, every key: fp32 within 1e-4 (measured 4.6e-5); bf16x3 / bf16x3f every value
+    within the north_star's 2e-3 and >= 95 % within 1e-4.  Their render() evaluates the coarse
+    net at fp32 (Network.mlp_dtype_for): with a split-bf16 coarse net one fine depth of the 4,096
+    was off by 3.4e-3 and four frame pixels by 2-6 uint8 levels, every one of them an importance
+    sample moved across a CDF bin by the coarse net's ~1e-5 relative error, which an exact
+    (fp64) MLP does not move by more than 1.4e-4 (tools/fullframe_conditioning.py,
+    profiles/r5/fullframe_conditioning.json); bf16 (operands rounded to bf16): >= 95 % within 2e-3,
+    its documented non-conforming tier (DESIGN.md section 5);
+  * every row sum within 800 x the per-value bound (so every row of the frame is covered, not
+    only the sampled rays);
+  * the uint8 frame (clip(rgb) x 255, truncated): fp32 / bf16x3 / bf16x3f every pixel within
+    one level (an error below 1/255 moves a truncated value by at most one level), >= 99.9 %
+    identical;
   * the march's MLP query count over the frame: within 16 of the reference's 12,383,297
     (measured: fp32 -2, bf16x3 +2; the 256-ray count of test_gpu_trained.py is exact).  A ray
     stops after the first queried step whose transmittance falls below 1e-4
@@ -39,9 +43,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 H = W = 800
 RENDER_KEYS = ["rgb_map_c", "depth_map_c", "acc_map_c", "rgb_map_f", "depth_map_f", "acc_map_f"]
 MARCH_KEYS = ["rgb_map_f", "depth_map_f", "acc_map_f"]
-TOL = {"fp32": 1e-4, "bf16x3": 1e-4, "bf16x3f": 1e-4}
-MAXERR = {"fp32": 1e-4, "bf16x3": 5e-3, "bf16x3f": 5e-3}
 CONTRACT = 2e-3  # north_star: rgb/depth within 2e-3 for an MLP below fp32
+# per tier: (tol, fraction of values within tol, bound on every value, uint8 frame: max levels,
+# fraction identical)
+BOUNDS = {"fp32": (1e-4, 1.0, 1e-4, 1, 0.999),
+          "bf16x3": (1e-4, 0.95, CONTRACT, 1, 0.999),
+          "bf16x3f": (1e-4, 0.95, CONTRACT, 1, 0.999),
+          "bf16": (CONTRACT, 0.95, 1.0, 255, 0.94)}  # (measured: 97.8-99.5 % within 2e-3, frame 95.4 % identical)
+TIERS = list(BOUNDS)
 
 
 @pytest.fixture(scope="module")
@@ -77,7 +86,7 @@ def renderer(cuda):
 
 def _compare(out, g4, prefix, keys, dtype):
     pix = torch.from_numpy(g4["pix"]).to(out[keys[0]].device)
-    tol, maxerr = TOL[dtype], MAXERR[dtype]
+    tol, frac_min, maxerr, max_levels, ident_min = BOUNDS[dtype]
     report = {}
     for k in keys:
         full = out[k]
@@ -86,27 +95,23 @@ def _compare(out, g4, prefix, keys, dtype):
         err = np.abs(got.astype(np.float64) - ref)
         frac = float((err <= tol).mean())
         report[k] = (float(err.max()), frac, float((err <= CONTRACT).mean()))
-        assert err.max() <= maxerr and frac >= (1.0 if dtype == "fp32" else 0.95), (prefix, k, dtype, err.max(), frac)
-        if dtype != "fp32":
-            assert (err <= CONTRACT).mean() >= 0.999, (prefix, k, dtype, (err <= CONTRACT).mean())
+        assert err.max() <= maxerr and frac >= frac_min, (prefix, k, dtype, err.max(), frac)
         rows = full.double().reshape(H, W, -1).sum(1).cpu().numpy()
         rref = g4[f"{prefix}_rowsum_{k}"].reshape(H, -1)
         rerr = float(np.abs(rows - rref).max())
         report[k] += (rerr,)
-        assert rerr <= W * maxerr, (prefix, k, dtype, rerr)
+        if dtype != "bf16":
+            assert rerr <= W * maxerr, (prefix, k, dtype, rerr)
     print(f"\n{prefix} {dtype}: " + ", ".join(f"{k} max {m:.1e} (<= 1e-4: {f:.4f}, <= 2e-3: {c:.4f}, row {r:.1e})"
                                            for k, (m, f, c, r) in report.items()))
     img = (out["rgb_map_f"].clamp(0, 1) * 255).to(torch.uint8).reshape(H, W, 3).cpu().numpy()
     d = np.abs(img.astype(int) - g4[f"{prefix}_frame_u8"].astype(int))
     print(f"{prefix} {dtype} uint8 frame: max {d.max()}, identical {(d == 0).mean():.5f}, "
           f"within one level {(d <= 1).mean():.6f}, pixels off by > 1: {int((d.max(-1) > 1).sum())}")
-    if dtype == "fp32":
-        assert d.max() <= 1 and (d == 0).mean() >= 0.999
-    else:  # (measured: max 6 levels, 99.981 % identical -- a few silhouette / chaotic pixels)
-        assert d.max() <= 8 and (d == 0).mean() >= 0.9995
+    assert d.max() <= max_levels and (d == 0).mean() >= ident_min, (prefix, dtype, d.max(), (d == 0).mean())
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16x3f"])
+@pytest.mark.parametrize("dtype", TIERS)
 def test_config2_full_frame_render(g4, frame, renderer, dtype):
     """Config 2: the 800x800 frame through Renderer.render (262,144-ray render chunks)."""
     net, r = renderer
@@ -117,7 +122,7 @@ def test_config2_full_frame_render(g4, frame, renderer, dtype):
     _compare(out, g4, "render", RENDER_KEYS, dtype)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16x3f"])
+@pytest.mark.parametrize("dtype", TIERS)
 def test_config4_full_frame_march(g4, frame, renderer, dtype):
     """Config 4: the frame through render_accelerated on the reference's res-128 bake of the
     same weights; the MLP query count over all 640,000 rays against the reference's."""
@@ -134,4 +139,4 @@ def test_config4_full_frame_march(g4, frame, renderer, dtype):
     _compare(out, g4, "march", MARCH_KEYS, dtype)
     ref_q = int(g4["march_queried"])
     print(f"march {dtype}: queried {out['n_queried']} (reference {ref_q}), evaluated {out['n_evaluated']}")
-    assert abs(out["n_queried"] - ref_q) <= 16
+    assert abs(out["n_queried"] - ref_q) <= (16 if dtype != "bf16" else ref_q // 1000)  # (bf16 measured +3,979)

@@ -738,13 +738,17 @@ def test_mlp_fwd_count_matches_fwd(cuda, ops, seeded_state, dtype):
         assert bool(torch.isnan(raw[n:]).all())  # nothing past the device count is written
 
 
+@pytest.mark.parametrize("Sc,Ni", [(64, 128), (63, 128), (33, 64), (3, 7), (17, 1)])
 @pytest.mark.parametrize("det", [True, False])
-def test_composite_pdf_fused_equals_separate(cuda, ops, det):
+def test_composite_pdf_fused_equals_separate(cuda, ops, det, Sc, Ni):
     """ops.composite_sample_pdf (one launch: coarse compositing + importance sampling + merge,
     the weights handed over in registers) is bit-identical to composite() then sample_pdf(),
-    forward and backward (volume_renderer.py:197-221)."""
-    g = torch.Generator().manual_seed(41)
-    R, Sc, Ni = 1000, 64, 128
+    forward and backward (volume_renderer.py:197-221).  Every coarse-sample count the renderer
+    sends to the fused kernel (3 <= Sc <= 64): Sc < 64 leaves lanes Sc..63 without a sample (the
+    l < Sc guard; the weight shuffled from lane l + 1 is used only for l < Sc - 2), and Ni down
+    to one importance sample."""
+    g = torch.Generator().manual_seed(41 + Sc + Ni)
+    R = 1000
     o = torch.randn(R, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, 4.0])
     d = torch.nn.functional.normalize(torch.randn(R, 3, generator=g), dim=-1) * 1.3
     rays = torch.cat([o, d], 1).to(cuda)

@@ -85,7 +85,7 @@ def test_trajectory_fp32_vs_oracle(cuda):
         assert abs(a - b) < 1e-4, free
 
 
-@pytest.mark.parametrize("steps,every", [(int(os.environ.get("NERF_PSNR_STEPS", "2000")), 500)])
+@pytest.mark.parametrize("steps,every", [(int(os.environ.get("NERF_PSNR_STEPS", "2000")), 250)])
 def test_psnr_fp32_vs_bf16_training(cuda, steps, every):
     from nerf_amd import ops
     from src.config import cfg
@@ -154,11 +154,12 @@ def test_psnr_fp32_vs_bf16_training(cuda, steps, every):
     # differences of +-0.6 dB, either sign, were measured: profiles/r2/psnr_fp32_vs_bf16.json)
     for dt in ("fp32",) + low:
         assert curve[dt][-1][1] > curve[dt][0][1] + 3.0, summary
-    # bf16's 4-checkpoint mean moves with any bit-level change of its trajectory (a different
-    # dW summation order): -0.33 / +0.18 (round 2), -0.47 (round 3), +0.05 / -0.53 (round 4,
-    # before / after the chunked backward, whose gradients hold the same tolerances); the 200k-step
-    # config-3 runs put bf16 +0.23 dB from fp32, inside its own 0.47 dB seed-to-seed spread
-    assert abs(summary["mean_delta_db"]) <= 0.8, summary
+    # The mean over 8 checkpoints (every 250 steps; rounds 2-4 used 4, every 500) of the shipped
+    # default configuration.  The 4-checkpoint bf16 mean moved with any bit-level change of its
+    # trajectory: -0.33 / +0.18 (round 2), -0.47 (round 3), +0.05 (round 4 default), and -0.53
+    # with the opt-in chunked backward (off by default, not what this test runs); the 200k-step
+    # config-3 runs put bf16 +0.23 dB from fp32, inside its own 0.47 dB seed-to-seed spread.
+    assert abs(summary["mean_delta_db"]) <= 0.5, summary
     assert abs(summary["mean_delta_db_bf16x3"]) <= 0.5, summary
 
 

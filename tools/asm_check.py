@@ -3,7 +3,8 @@
     layout tables would show up as one),
   * every counted `s_waitcnt vmcnt(N)` + s_barrier hand-off waits for the weight DMA:
     N <= vector-memory ops issued after the last global_load_lds before it,
-  * no scratch (spills).
+  * no scratch (spills),
+  * no compiler code touches M0 (the lean LDS-DMA sets it without saving it).
     python tools/asm_check.py            (exit status 1 on a violation)
 """
 import os
@@ -60,6 +61,16 @@ def check(asm):
         loops = [i for i, l in enumerate(lines) for m in [re.search(r"s_(?:cbranch_\w+|branch)\s+(\.LBB\w+)", l)]
                  if m and m.group(1) in labels and labels[m.group(1)] < i]
         since, waits, unsafe = None, 0, 0
+        # the lean LDS-DMA (NERF_DMA_LEAN) writes M0 without saving it: no compiler code of the
+        # kernel may read or write M0 (every M0 access must sit inside an inline-asm statement)
+        in_asm, m0_outside = False, 0
+        for l in lines:
+            if ";;#ASMSTART" in l:
+                in_asm = True
+            elif ";;#ASMEND" in l:
+                in_asm = False
+            elif not in_asm and re.search(r"\bm0\b", l) and not l.strip().startswith(";"):
+                m0_outside += 1
         for i, l in enumerate(lines):
             t = l.strip()
             if t.startswith("global_load_lds"):
@@ -74,9 +85,10 @@ def check(asm):
         # loop (+ its guard) is its only backward branch
         persist = re.search(r"fwd_kernel\w*?ELb0ELb0ELb1E", name) is not None
         straight = "dw_kernel" in name or "dw_reduce" in name or not loops or (persist and len(loops) <= 2)
-        ok = straight and not unsafe
+        ok = straight and not unsafe and not m0_outside
         bad += not ok
-        print(f"{'ok ' if ok else 'BAD'} {name[:70]:70s} loops={len(loops)} counted_waits={waits} unsafe={unsafe}")
+        print(f"{'ok ' if ok else 'BAD'} {name[:70]:70s} loops={len(loops)} counted_waits={waits} unsafe={unsafe} "
+              f"m0_outside_asm={m0_outside}")
     for m in re.finditer(r"\.name:\s+(\S+)\n(?:.*\n){0,40}?\s+\.private_segment_fixed_size:\s+(\d+)", asm):
         if int(m.group(2)):
             bad += 1
