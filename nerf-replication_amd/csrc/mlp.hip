@@ -30,11 +30,6 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 
-// (NERF_DIAG_EPI: diagnostic timing builds only -- the bf16x3 finish without its ReLU, mask bits
-// and lo half, results meaningless -- to price the epilogue in the kernels' time)
-#ifndef NERF_DIAG_EPI
-#define NERF_DIAG_EPI 0
-#endif
 // mask bits of the bf16x3 training forward from the packed hi pair (v_pk_min_u16 + v_lshl_or_b32
 // per register pair) instead of per-value compares and selects
 #ifndef NERF_PACKED_MASK
@@ -218,7 +213,7 @@ struct PBF3 {
     const uint32_t hw = pack_bf16(x0, x1);
     const uint32_t lw = pack_bf16(x0 - __uint_as_float(hw << 16), x1 - __uint_as_float(hw & 0xffff0000u));
     put(t.hi[k >> 2], k & 3, hw);
-    put(t.lo[k >> 2], k & 3, NERF_DIAG_EPI ? 0u : lw);
+    put(t.lo[k >> 2], k & 3, lw);
   }
 };
 
@@ -347,6 +342,11 @@ typedef __attribute__((address_space(3))) void lds_void;
 #endif
 #ifndef NERF_DIAG_NO_STORE
 #define NERF_DIAG_NO_STORE 0
+#endif
+// (NERF_DIAG_STAMPS: diagnostic only -- the forward overwrites two raw rows per workgroup with its CU id and
+// entry / prologue-done / end timestamps, tools/wg_stamps.py)
+#ifndef NERF_DIAG_STAMPS
+#define NERF_DIAG_STAMPS 0
 #endif
 __device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t lds_wave_base) {
   if constexpr (NERF_DIAG_NO_DMA) return;
@@ -525,11 +525,10 @@ constexpr int FINISH_DELAY = NERF_FINISH_DELAY;
 // Cross-group finish: the last unit of a group is finished after the barrier.  Not in the
 // bf16x3 forward: a finished accumulator carried over the barrier (plus the hi / lo split of
 // the finish) takes it past 512 VGPRs (139 spilled); finished in-group it needs none.
-#ifndef NERF_CROSS_FINISH_BF3_FWD
-#define NERF_CROSS_FINISH_BF3_FWD 0
-#endif
+// (r5: with the lean DMA and packed masks the bf16x3 forward fits cross-group finish without spills, 372
+// VGPRs, but it is not faster: bf16x3f training forward 1.609 vs 1.599 ms)
 template <class P, int DIR> __host__ __device__ constexpr bool cross_finish() {
-  return NERF_CROSS_FINISH_BF3_FWD || !(P::KIND == K_BF16X3 && DIR == 0);
+  return !(P::KIND == K_BF16X3 && DIR == 0);
 }
 // the unit finished inside group g: (first, last] = units whose finish is issued in g.
 // With cross_finish() the last unit of a group is finished FINISH_DELAY steps into the
@@ -1011,8 +1010,6 @@ struct FwdWave {
             bits |= (a1 > 0.f ? 1u : 0u) << mask_bit(2 * k + 1);
           }
           P::set_dword(out, k, d);
-        } else if constexpr (P::KIND == K_BF16X3 && NERF_DIAG_EPI) {
-          P::set_pair(out, k, a0, a1);
         } else {
           // ReLU as an integer max on the float bits (negative floats are negative ints)
           const int y0 = max(__float_as_int(a0), 0), y1 = max(__float_as_int(a1), 0);
@@ -1113,6 +1110,9 @@ struct FwdWave {
   }
 
   __device__ __forceinline__ void run() {
+#if NERF_DIAG_STAMPS
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int64_t ms = m < a.M ? m : a.M - 1;
     px = a.pts[ms * 3 + 0];
     py = a.pts[ms * 3 + 1];
@@ -1142,12 +1142,28 @@ struct FwdWave {
       }();
       wait_barrier<N0>();
     }
+#if NERF_DIAG_STAMPS
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+#endif
     settle(dx);
     settle(dy);
     settle(dz);
     sfor<GT::t.n>([&](auto gg) { step<decltype(gg)::value>(); });
     if (h == 0 && m < a.M)
       *(float4*)(a.raw + m * 4) = DENSITY ? make_float4(0.f, 0.f, 0.f, alpha) : make_float4(rgb0, rgb1, rgb2, alpha);
+#if NERF_DIAG_STAMPS
+    // (diagnostic only) wave 0 lane 0 of each workgroup overwrites raw rows 0-1 of its block:
+    // hw id, xcc id, entry / prologue-done / end (s_memrealtime)
+    const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+    if (wave == 0 && lane == 0) {
+      uint32_t* d = (uint32_t*)(a.raw + (wblock * 32) * 4);
+      d[0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      d[1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+      d[2] = (uint32_t)t0, d[3] = (uint32_t)(t0 >> 32);
+      d[4] = (uint32_t)t1, d[5] = (uint32_t)(t1 >> 32);
+      d[6] = (uint32_t)t2, d[7] = (uint32_t)(t2 >> 32);
+    }
+#endif
   }
 };
 
