@@ -31,6 +31,7 @@ extern "C" {
 #define NERF_DTYPE_BF16 1
 #define NERF_DTYPE_BF16X3 2 /* fp32 operands split into bf16 hi + lo: three bf16 MFMAs per product */
 #define NERF_DTYPE_BF16X3F 3 /* the bf16x3 forward (outputs bit-identical to bf16x3) + the bf16 backward */
+#define NERF_DTYPE_BF16X6 4  /* inference forward only: operands split into three bf16, six products */
 
 #define NERF_MLP_STORE 1   /* keep activations + ReLU masks for backward */
 #define NERF_MLP_DENSITY 2 /* sigma only (grid bake) */
@@ -119,7 +120,9 @@ int nerf_mse2_bwd(const float* c, const float* f, const float* gt, int64_t n, co
  * 3 = bf16x3f: the bf16x3 forward (its outputs are bf16x3's, bit for bit) whose training stores are
  * the bf16 (hi) halves, and the bf16 backward (dX chain, dW).  Every function maps 3 to its part:
  * packed_bytes / pack dir 0 and fwd -> bf16x3, pack dir 1 / act / dz bytes / bwd -> bf16.
- * Any other dtype: the size helpers return -1, every launching function -22 (nerf_last_error
+ * 4 = bf16x6, an inference forward only (x = hi + mid + lo, products hh hm mh hl lh mm, fp32 accumulation:
+ * at least as accurate as fp32): packed_bytes / pack dir 0 and nerf_mlp_fwd with flags 0; everything else
+ * rejects it.  Any other dtype: the size helpers return -1, every launching function -22 (nerf_last_error
  * names the dtype). */
 int64_t nerf_mlp_net_params(void);
 int64_t nerf_mlp_param_offset(int i);

@@ -44,7 +44,7 @@ __device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
 // ------------------------------------------------------------------------------------
 // precision policies
 // ------------------------------------------------------------------------------------
-enum PKind { K_F32 = 0, K_BF16 = 1, K_BF16X3 = 2 };
+enum PKind { K_F32 = 0, K_BF16 = 1, K_BF16X3 = 2, K_BF16X6 = 3 };
 
 struct PF32 {
   static constexpr int KIND = K_F32;
@@ -214,6 +214,70 @@ struct PBF3 {
     const uint32_t lw = pack_bf16(x0 - __uint_as_float(hw << 16), x1 - __uint_as_float(hw & 0xffff0000u));
     put(t.hi[k >> 2], k & 3, hw);
     put(t.lo[k >> 2], k & 3, lw);
+  }
+};
+
+// bf16x6 (inference forward only, round 5): every fp32 operand split exactly into three bf16,
+// x = hi + mid + lo (24 significant bits), and the six products hh, hm, mh, hl, lh, mm accumulated in
+// fp32 on the bf16 MFMA (the dropped ml, lm, ll are < 2^-24 relative): at least as accurate as an fp32
+// GEMM, at 6 bf16 MFMAs (192 cycles) per K = 16 step instead of 8 fp32 ones (512).  The render of the
+// bf16x3 tiers evaluates its COARSE net with it (Network.mlp_dtype_for): a split-bf16 coarse net moves
+// importance samples across CDF bins.  Activations stay fp32 in registers (16
+// VGPRs per tile, as PF32) and are split when a K half is used (12 VGPRs live at a time): the chunk
+// order hi, mid, lo of K half 0, then of K half 1, so the split of one half is reused by its three
+// chunks.  Weights: chunk 3q + p = part p (hi / mid / lo) of K half q.
+struct PBF6 {
+  static constexpr int KIND = K_BF16X6;
+  static constexpr int CH = 6;
+  static constexpr int E = 8;
+  static constexpr int WAVES = 4;  // one wave per SIMD (16-VGPR fp32 tiles)
+  static constexpr int ESIZE = 4;
+  static constexpr int SPL = 8;
+  static constexpr int PE = 2;  // PE_POLY: fp32-accurate to 1.6 ulp
+  using Store = __bf16;
+  struct Tile { float v[16]; };
+  struct Split { bf16x8 h, m, l; };
+  // K half q (registers 8q .. 8q + 7) as three bf16x8 parts
+  static __device__ __forceinline__ Split split(const Tile& t, int q) {
+    uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x0 = t.v[8 * q + 2 * k], x1 = t.v[8 * q + 2 * k + 1];
+      hw[k] = pack_bf16(x0, x1);
+      const float r0 = x0 - __uint_as_float(hw[k] << 16), r1 = x1 - __uint_as_float(hw[k] & 0xffff0000u);
+      mw[k] = pack_bf16(r0, r1);
+      lw[k] = pack_bf16(r0 - __uint_as_float(mw[k] << 16), r1 - __uint_as_float(mw[k] & 0xffff0000u));
+    }
+    return Split{__builtin_bit_cast(bf16x8, make_uint4(hw[0], hw[1], hw[2], hw[3])),
+                 __builtin_bit_cast(bf16x8, make_uint4(mw[0], mw[1], mw[2], mw[3])),
+                 __builtin_bit_cast(bf16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]))};
+  }
+  static __device__ __forceinline__ f32x16 mma(uint4 a, const Tile& b, int c, f32x16 acc) {
+    const bf16x8 av = __builtin_bit_cast(bf16x8, a);
+    const int q = c / 3, p = c % 3;
+    const Split x = split(b, q);  // (identical for the three chunks of a half: CSE'd)
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, x.h, acc, 0, 0, 0);
+    if (p == 2) return acc;                                                  // lo . hi
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, x.m, acc, 0, 0, 0);   // . mid
+    if (p == 1) return acc;
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, x.l, acc, 0, 0, 0);  // hi . lo
+  }
+  static __device__ __forceinline__ void set(Tile& t, int rho, float x) { t.v[rho] = x; }
+  static __device__ __forceinline__ void pack16(Tile& t, const float (&v)[16]) {
+#pragma unroll
+    for (int rho = 0; rho < 16; ++rho) t.v[rho] = v[rho];
+  }
+  static __device__ __forceinline__ float get(const Tile& t, int rho) { return t.v[rho]; }
+  static __host__ __device__ constexpr int rho_of(int c, int e) { return (c / 3) * E + e; }
+  static __device__ __forceinline__ Store cvt_c(float x, int c) {
+    const __bf16 h = (__bf16)x;
+    const float r = x - (float)h;
+    const __bf16 m = (__bf16)r;
+    return c % 3 == 0 ? h : c % 3 == 1 ? m : (__bf16)(r - (float)m);
+  }
+  static __device__ __forceinline__ void set_pair(Tile& t, int k, float x0, float x1) {
+    t.v[2 * k] = x0;
+    t.v[2 * k + 1] = x1;
   }
 };
 
@@ -2126,6 +2190,15 @@ void mlp_dw_impl(const DwArgs& w, dim3 grid, hipStream_t stream) {
 NERF_MLP_IMPLS(extern, PF32)
 NERF_MLP_IMPLS(extern, PBF16)
 NERF_MLP_IMPLS(extern, PBF3)
+NERF_MLP_I_FWDI(extern, PBF6)  // bf16x6: the inference forward and its pack only
+NERF_MLP_I_PACK(extern, PBF6)
+#elif NERF_MLP_PREC == 3
+#if !defined(NERF_MLP_PART) || NERF_MLP_PART == 1
+NERF_MLP_I_FWDI(, PBF6)
+#endif
+#if !defined(NERF_MLP_PART) || NERF_MLP_PART == 2
+NERF_MLP_I_PACK(, PBF6)
+#endif
 #else
 #if NERF_MLP_PREC == 0
 #define NERF_PP PF32
@@ -2169,9 +2242,12 @@ int64_t nerf_mlp_param_offset(int i) { return (i >= 0 && i <= NPARAM) ? param_of
 static int fwd_prec(int dtype) { return dtype == 3 ? 2 : dtype; }
 static int bwd_prec(int dtype) { return dtype == 3 ? 1 : dtype; }
 static int store_prec(int dtype) { return dtype == 3 ? 1 : dtype; }
+// dtype 4 (bf16x6) is an inference forward only: its forward pack and nerf_mlp_fwd without flags
+static bool train_dtype(int dtype) { return dtype >= 0 && dtype <= 3; }
 
 int64_t nerf_mlp_packed_bytes(int dtype, int dir) {
-  if (dtype < 0 || dtype > 3 || (dir != 0 && dir != 1)) return -1;
+  if (dtype == 4) return dir == 0 ? total_chunks(PBF6::CH, 0) * 1024 : -1;
+  if (!train_dtype(dtype) || (dir != 0 && dir != 1)) return -1;
   const int p = dir == 0 ? fwd_prec(dtype) : bwd_prec(dtype);
   return total_chunks(p == 1 ? PBF16::CH : PF32::CH, dir) * 1024;  // bf16x3: CH 4 as fp32
 }
@@ -2189,8 +2265,9 @@ int64_t nerf_mlp_mask_bytes(int64_t M) { return nerf_mlp_padded_samples(M) / 32 
 
 int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void* packed_bwd, hipStream_t stream) {
   NERF_REQUIRE(params != nullptr, "nerf_mlp_pack: params is null");
-  NERF_REQUIRE(dtype >= 0 && dtype <= 3,
-               "nerf_mlp_pack: dtype must be 0 (f32), 1 (bf16), 2 (bf16x3) or 3 (bf16x3f), got %d", dtype);
+  NERF_REQUIRE(dtype >= 0 && dtype <= 4,
+               "nerf_mlp_pack: dtype must be 0 (f32), 1 (bf16), 2 (bf16x3), 3 (bf16x3f) or 4 (bf16x6), got %d", dtype);
+  NERF_REQUIRE(dtype != 4 || packed_bwd == nullptr, "nerf_mlp_pack: dtype 4 (bf16x6) has no backward pack");
   ParamPtrs prm;
   for (int i = 0; i < NPARAM; ++i) {
     NERF_REQUIRE(params[i] != nullptr, "nerf_mlp_pack: params[%d] is null", i);
@@ -2200,7 +2277,8 @@ int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void*
     void* dst = dir == 0 ? packed_fwd : packed_bwd;
     if (!dst) continue;
     const int p = dir == 0 ? fwd_prec(dtype) : bwd_prec(dtype);
-    if (p == 0) mlp_pack_impl<PF32>(prm, dir, (char*)dst, stream);
+    if (p == 4) mlp_pack_impl<PBF6>(prm, dir, (char*)dst, stream);
+    else if (p == 0) mlp_pack_impl<PF32>(prm, dir, (char*)dst, stream);
     else if (p == 1) mlp_pack_impl<PBF16>(prm, dir, (char*)dst, stream);
     else mlp_pack_impl<PBF3>(prm, dir, (char*)dst, stream);
     if (int e = check_launch("nerf_mlp_pack")) return e;
@@ -2212,7 +2290,8 @@ int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void*
 int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const float* viewdirs, int samples_per_dir,
                  const int32_t* dir_index, int64_t M, int flags, float* raw, void* act, uint16_t* masks,
                  hipStream_t stream) {
-  NERF_REQUIRE(dtype >= 0 && dtype <= 3, "nerf_mlp_fwd: bad dtype %d", dtype);
+  NERF_REQUIRE(dtype >= 0 && dtype <= 4, "nerf_mlp_fwd: bad dtype %d", dtype);
+  NERF_REQUIRE(dtype != 4 || flags == 0, "nerf_mlp_fwd: dtype 4 (bf16x6) is an inference forward only (flags 0)");
   NERF_REQUIRE(M >= 0, "nerf_mlp_fwd: M < 0");
   if (M == 0) return 0;
   const bool store = flags & 1, density = flags & 2;
@@ -2229,7 +2308,8 @@ int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const floa
     else if (dtype == 2) mlp_fwd_train_impl<PBF3>(a, stream);
     else mlp_fwd_train_half_impl(a, stream);
   } else {
-    if (dtype == 0) mlp_fwd_infer_impl<PF32>(a, density, stream);
+    if (dtype == 4) mlp_fwd_plain_impl<PBF6>(a, stream);
+    else if (dtype == 0) mlp_fwd_infer_impl<PF32>(a, density, stream);
     else if (dtype == 1) mlp_fwd_infer_impl<PBF16>(a, density, stream);
     else mlp_fwd_infer_impl<PBF3>(a, density, stream);
   }

@@ -24,14 +24,16 @@ import torch
 
 from ._lib import check, lib, ptr, stream_of
 
-F32, BF16, BF16X3, BF16X3F = 0, 1, 2, 3
+F32, BF16, BF16X3, BF16X3F, BF16X6 = 0, 1, 2, 3, 4
 # bf16x3: fp32 operands split into bf16 hi + lo, products hi*hi + hi*lo + lo*hi on the bf16
 # MFMA with fp32 accumulation (csrc/mlp.hip PBF3): fp32-class results at bf16-MFMA cost x3.
 # bf16x3f: the bf16x3 forward (outputs identical to bf16x3's) with the bf16 backward (its
 # training stores are the bf16 hi halves): bf16x3 outputs, bf16 gradients
+# bf16x6: an inference forward only -- operands split exactly into three bf16, six products (at least
+# as accurate as fp32): the coarse net of a bf16x3 / bf16x3f render (Network.mlp_dtype_for)
 DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16, "bf16x3": BF16X3,
-          "bf16x3f": BF16X3F}
-DTYPE_NAMES = {F32: "fp32", BF16: "bf16", BF16X3: "bf16x3", BF16X3F: "bf16x3f"}
+          "bf16x3f": BF16X3F, "bf16x6": BF16X6}
+DTYPE_NAMES = {F32: "fp32", BF16: "bf16", BF16X3: "bf16x3", BF16X3F: "bf16x3f", BF16X6: "bf16x6"}
 
 
 def pack_code(dtype: int, direction: int) -> int:
@@ -48,7 +50,7 @@ def dtype_code(d) -> int:
     if isinstance(d, int):
         return d
     if d not in DTYPES:
-        raise ValueError(f"unsupported MLP dtype {d!r} (fp32, bf16, bf16x3 or bf16x3f)")
+        raise ValueError(f"unsupported MLP dtype {d!r} (fp32, bf16, bf16x3, bf16x3f or the inference-only bf16x6)")
     return DTYPES[d]
 
 
@@ -539,6 +541,8 @@ class _MLP(torch.autograd.Function):
         M = pts.shape[0]
         dev = pts.device
         store = bool(want_grad) and any(ctx.needs_input_grad[8:])
+        if dtype == BF16X6 and (store or density_only):
+            raise RuntimeError("the bf16x6 MLP is an inference forward only (no autograd, no density-only pass)")
         raw = torch.empty(M, 4, device=dev, dtype=torch.float32)
         if M == 0:
             ctx.M = 0

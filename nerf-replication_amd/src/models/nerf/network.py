@@ -77,10 +77,13 @@ class Network(nn.Module):
         split-bf16 coarse MLP (~1e-5 relative per dot product) moves a sample across a CDF bin
         on a few rays of an 800x800 frame -- fine depth off by up to 3.7e-2 -- where an exact MLP
         moves them by < 1.4e-4 (tools/fullframe_conditioning.py, profiles/r5/).  With the fp32
-        coarse pass every value of the frame holds the north_star's 2e-3.  The training forward
-        (autograd) keeps bf16x3: at perturb 1 the importance samples are random draws from the
-        CDF, which a 1e-5 relative perturbation leaves distributed the same.
-        task_arg.coarse_inference_dtype (default fp32) overrides the choice."""
+        coarse pass every value of the frame holds the north_star's 2e-3 (tests/test_gpu_fullframe.py).
+        The training forward (autograd) keeps bf16x3: at perturb 1 the importance samples are
+        random draws from the CDF, which a 1e-5 relative perturbation leaves distributed the same.
+        task_arg.coarse_inference_dtype (default fp32) overrides the choice; "bf16x6" (operands
+        split exactly into three bf16, six products: fp32-class, faster than the fp32 MFMA) holds
+        2e-3 on the 4,096 sampled rays but leaves one frame pixel 2 uint8 levels off, so it is not
+        the default."""
         dt = self.mlp_dtype
         if model != "fine" and dt in ("bf16x3", "bf16x3f"):
             recording = torch.is_grad_enabled() and any(p.requires_grad for p in fn.parameters())

@@ -83,7 +83,8 @@ def test_bf16x3f_dtype_maps_to_its_parts(lib):
     (nerf_amd.h: "Every function maps 3 to its part")."""
     text = open(HEADER).read()
     codes = dict(re.findall(r"#define (NERF_DTYPE_\w+) (\d+)", text))
-    assert codes == {"NERF_DTYPE_F32": "0", "NERF_DTYPE_BF16": "1", "NERF_DTYPE_BF16X3": "2", "NERF_DTYPE_BF16X3F": "3"}
+    assert codes == {"NERF_DTYPE_F32": "0", "NERF_DTYPE_BF16": "1", "NERF_DTYPE_BF16X3": "2", "NERF_DTYPE_BF16X3F": "3",
+                     "NERF_DTYPE_BF16X6": "4"}
     assert lib.nerf_mlp_packed_bytes(3, 0) == lib.nerf_mlp_packed_bytes(2, 0)
     assert lib.nerf_mlp_packed_bytes(3, 1) == lib.nerf_mlp_packed_bytes(1, 1)
     for M in (1, 4097, 786432):
@@ -91,7 +92,30 @@ def test_bf16x3f_dtype_maps_to_its_parts(lib):
         assert lib.nerf_mlp_dz_bytes(3, M) == lib.nerf_mlp_dz_bytes(1, M)
 
 
-@pytest.mark.parametrize("dtype", [-1, 4, 7])
+def test_bf16x6_is_an_inference_forward_only(lib):
+    """NERF_DTYPE_BF16X6 (4): a forward pack and an inference forward; no backward pack, no training
+    stores, no backward, no device-count forward."""
+    import ctypes
+    from nerf_amd._lib import check
+    # six 1 KiB chunks per 32-feature input tile (hi, mid, lo of each K half) against fp32's four, + the bias chunks
+    p4, p0, p1 = (lib.nerf_mlp_packed_bytes(d, 0) for d in (4, 0, 1))
+    assert p4 % 1024 == 0 and p4 - p0 == p0 - p1
+    assert lib.nerf_mlp_packed_bytes(4, 1) == -1
+    assert lib.nerf_mlp_act_bytes(4, 256) == -1 and lib.nerf_mlp_dz_bytes(4, 256) == -1
+    params = ctypes.cast((ctypes.c_void_p * 24)(*([None] * 24)), ctypes.c_void_p)
+    dummy = ctypes.c_void_p(16)
+    with pytest.raises(RuntimeError, match="backward pack"):
+        check(lib.nerf_mlp_pack(params, 4, None, dummy, None), "nerf_mlp_pack")
+    for flags in (1, 2):
+        with pytest.raises(RuntimeError, match="inference forward only"):
+            check(lib.nerf_mlp_fwd(None, 4, None, None, 1, None, 10, flags, None, None, None, None), "nerf_mlp_fwd")
+    with pytest.raises(RuntimeError, match="dtype"):
+        check(lib.nerf_mlp_bwd_dx(None, 4, None, 10, None, None, None), "nerf_mlp_bwd_dx")
+    with pytest.raises(RuntimeError, match="dtype"):
+        check(lib.nerf_mlp_fwd_count(None, 4, None, None, 1, None, None, 10, None, None), "nerf_mlp_fwd_count")
+
+
+@pytest.mark.parametrize("dtype", [-1, 5, 7])
 def test_bad_dtype_is_rejected_everywhere(lib, dtype):
     """Every MLP entry point refuses a dtype outside 0..3 before touching any pointer (no GPU
     needed: the argument checks run first)."""
@@ -152,4 +176,4 @@ def test_bf16x3f_through_the_c_abi(cuda, seeded_state):
     assert torch.equal(hi, out[3][3])
     raw = torch.empty(M, 4, device=cuda)
     with pytest.raises(RuntimeError, match="dtype"):
-        check(L.nerf_mlp_fwd(ptr(out[3][0]), 4, ptr(pts), ptr(vd), spd, None, M, 0, ptr(raw), None, None, s), "fwd")
+        check(L.nerf_mlp_fwd(ptr(out[3][0]), 5, ptr(pts), ptr(vd), spd, None, M, 0, ptr(raw), None, None, s), "fwd")

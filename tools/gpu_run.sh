@@ -2,7 +2,7 @@
 #   gpurun -- bash tools/gpu_run.sh STEP [STEP ...]
 # Steps (each under its own time limit; the script stops at the first failure):
 #   tests            the whole -m gpu suite
-#   tests=EXPR       -m gpu tests selected by -k EXPR
+#   tests=EXPR       -m gpu tests selected by -k EXPR (+ for spaces)
 #   file=PATH        -m gpu tests of one file
 #   smoke            __graft_entry__.smoke()
 #   bench            the default bench line (python bench.py)
@@ -38,7 +38,7 @@ nm=0
 for step in "$@"; do
   case "$step" in
     tests) run tests 1000 $PYT --maxfail=10 tests ;;
-    tests=*) nm=$((nm + 1)); run "tests_k$nm" 900 $PYT --maxfail=10 tests -k "${step#tests=}" ;;
+    tests=*) nm=$((nm + 1)); k=${step#tests=}; run "tests_k$nm" 900 $PYT --maxfail=10 tests -k "${k//+/ }" ;;
     file=*) f=${step#file=}; run "file_$(basename $f .py)" 900 $PYT --maxfail=10 "$f" ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) run bench 600 python3 -u bench.py ;;
