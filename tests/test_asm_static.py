@@ -27,7 +27,9 @@ def test_mlp_kernels_handoffs_and_registers(capsys):
                # bf16x3f: the bf16x3 training forward storing bf16 halves
                "fwd_kernel<nerf::mlp::PBF3, true, false, false, true>",
                # the persistent inference forwards of the grid march (device-side sample count)
-               "fwd_kernel<nerf::mlp::PF32, false, false, true>", "fwd_kernel<nerf::mlp::PBF16, false, false, true>"]
+               "fwd_kernel<nerf::mlp::PF32, false, false, true>", "fwd_kernel<nerf::mlp::PBF16, false, false, true>",
+               # bf16x6: the inference-only forward (three-way split on the fly)
+               "fwd_kernel<nerf::mlp::PBF6, false, false, false>"]
     with tempfile.TemporaryDirectory() as tmp:
         asm = asm_check.build_asm(tmp, kernels)
     asm_check.check(asm)
@@ -47,5 +49,5 @@ def test_mlp_kernels_handoffs_and_registers(capsys):
     assert re.search(r"ok  _ZN4nerf3mlp10fwd_kernelINS0_5PBF16ELb0ELb0ELb1E", out), "\n" + out
     for name in ("fwd_kernelINS0_5PBF16ELb1ELb0", "fwd_kernelINS0_4PF32ELb1ELb0", "dx_kernelINS0_4PF32",
                  "fwd_kernelINS0_4PBF3ELb1ELb0ELb0ELb0E", "dx_kernelINS0_4PBF3",
-                 "fwd_kernelINS0_4PBF3ELb1ELb0ELb0ELb1E"):
+                 "fwd_kernelINS0_4PBF3ELb1ELb0ELb0ELb1E", "fwd_kernelINS0_4PBF6ELb0ELb0ELb0E"):
         assert re.search(name + r".*counted_waits=\d+ unsafe=0", out), "\n" + out
