@@ -349,15 +349,17 @@ def _masked_mlp(p, x63, d27, mk):
     return torch.cat([F.linear(hv, *p["rgb_linear"]), alpha], -1)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3"])
 def test_pe_fused_tiles(cuda, ops, O, seeded_state, dtype):
     """a4 directly: the positional encoding the fused forward generates (freq.py:7-32), read back
     from its training store -- tiles AT_X 0-1 (PE(xyz), 63 features + 1 zero) and AT_D 2 (PE(dir),
     27 + 5 zero) of each 32-sample block, block-major, chunk c of 64 lanes x 16 B holding
-    registers 4c + e (fp32) / 8c + e (bf16), feature acc_row(rho, lane >> 5) of sample lane & 31
-    -- against the oracle's torch encoding of the same points.  fp32 (libm sincosf of the exact
-    x 2^k): within 2 ulp of 1.0 (2.4e-7), raw coordinates and padding exact; bf16 (v_sin_f32
-    after an f64 revolution reduction, then rounded to bf16): within bf16's relative half-ulp."""
+    registers 4c + e (fp32) / 8c + e (bf16; bf16x3: hi chunks, then lo), feature acc_row(rho,
+    lane >> 5) of sample lane & 31 -- against the oracle's torch encoding of the same points.  fp32
+    (libm sincosf of the exact x 2^k): within 2 ulp of 1.0 (2.4e-7), raw coordinates and padding
+    exact; bf16 (v_sin_f32 after an f64 revolution reduction, then rounded to bf16): within bf16's
+    relative half-ulp; bf16x3 (f64 revolution reduction + fp32 polynomial, split hi + lo): within
+    2^-16 relative."""
     from nerf_amd._lib import lib, ptr, stream_of
     M, spd = 20010, 10
     g = torch.Generator().manual_seed(21)
@@ -373,15 +375,18 @@ def test_pe_fused_tiles(cuda, ops, O, seeded_state, dtype):
     assert lib().nerf_mlp_fwd(ptr(packer.get(code, 0)), code, ptr(pc), ptr(vc), spd, None, M, 1, ptr(raw), ptr(act),
                               ptr(masks), stream_of(pc)) == 0
     torch.cuda.synchronize()
+    dirs = vd[:, None].expand(-1, spd, 3).reshape(-1, 3)[:M]
     if dtype == "fp32":
         v = act.view(torch.float32).cpu()
-        E = 4
+        E, CH = 4, 4
     else:
         v = act.view(torch.bfloat16).float().cpu()
-        E = 8
-    CH = 16 // E
-    nblk = v.numel() // (79 * 32 * 32)
+        E, CH = 8, (4 if dtype == "bf16x3" else 2)
+    nblk = v.numel() // (79 * 32 * 32 * (2 if dtype == "bf16x3" else 1))
     v = v.reshape(nblk, 79, CH, 64, E)[:, :3]                      # [blk, tile, c, lane, e]
+    if dtype == "bf16x3":                                           # hi (chunks 0, 1) + lo (2, 3)
+        v = v[:, :, :2] + v[:, :, 2:]
+        CH = 2
     dec = torch.zeros(nblk, 32, 96)                                 # [blk, sample, feature]
     for t in range(3):
         for c in range(CH):
@@ -391,7 +396,6 @@ def test_pe_fused_tiles(cuda, ops, O, seeded_state, dtype):
                     f = 32 * t + (rho & 3) + 8 * (rho >> 2) + 4 * h
                     dec[:, :, f] = v[:, t, c, 32 * h:32 * h + 32, e]
     dec = dec.reshape(-1, 96)[:M]
-    dirs = vd[:, None].expand(-1, spd, 3).reshape(-1, 3)[:M]
     ref_x, ref_d = O.positional_encoding(pts, 10), O.positional_encoding(dirs, 4)
     got_x, got_d = dec[:, :63], dec[:, 64:91]
     assert float(dec[:, 63].abs().max()) == 0 and float(dec[:, 91:].abs().max()) == 0   # padding
@@ -399,8 +403,10 @@ def test_pe_fused_tiles(cuda, ops, O, seeded_state, dtype):
         np.testing.assert_array_equal(got_x[:, :3].numpy(), ref_x[:, :3].numpy())
         np.testing.assert_array_equal(got_d[:, :3].numpy(), ref_d[:, :3].numpy())
         rtol, atol = 0.0, 2.4e-7
-    else:  # bf16's relative half-ulp (2^-9) of the rounded value, + v_sin_f32's ~1e-6
+    elif dtype == "bf16":  # bf16's relative half-ulp (2^-9) of the rounded value, + v_sin_f32's ~1e-6
         rtol, atol = 2.0 ** -8, 2e-6
+    else:  # hi + lo keeps 16 significant bits (2^-16 relative), + the polynomial's ~2 ulp
+        rtol, atol = 2.0 ** -16, 1e-6
     np.testing.assert_allclose(got_x.numpy(), ref_x.numpy(), rtol=rtol, atol=atol)
     np.testing.assert_allclose(got_d.numpy(), ref_d.numpy(), rtol=rtol, atol=atol)
 
@@ -714,7 +720,7 @@ def test_image_metrics_match_host_evaluator(cuda, ops, H, W, noise):
     assert abs(ssim - ref_ssim) < 1e-9, (ssim, ref_ssim)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16", "bf16x3f"])
 def test_mlp_dw_deterministic(cuda, ops, seeded_state, dtype):
     """dW with the workspace (per-item partials, fixed-order reduce) is bit-identical run to
     run and equal, to fp32 summation-order rounding, to the atomic accumulation."""

@@ -13,7 +13,7 @@ while [ $# -gt 1 ]; do
   B=/tmp/nerf_var_$name
   rm -rf $B; cp -rp $ROOT/build/nerf_amd $B; touch $B/*.o
   for o in $ONLY; do rm -f $B/$o.o; done
-  (make -C $CS -j4 BUILD=$B OUT=$ROOT/ab/$name.so EXTRA="$defs" > /tmp/nerf_var_$name.log 2>&1 || echo "FAILED $name") &
+  (make -C $CS -j${VJ:-4} BUILD=$B OUT=$ROOT/ab/$name.so EXTRA="$defs" > /tmp/nerf_var_$name.log 2>&1 || echo "FAILED $name") &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done

@@ -298,6 +298,19 @@ def compare(args):
     torch.cuda.synchronize()
     for name, _ in libs[1:]:
         out["identical_to_" + n0][name]["raw_inference"] = bool(torch.equal(bufs[name]["raw"], bufs[n0]["raw"]))
+    # and the deterministic dW of each build's own stores (the store layout may differ between builds;
+    # the gradient may not)
+    for name, L in libs:
+        b = bufs[name]
+        kernels(L, b)["fwd_train"]()
+        kernels(L, b)["dx"]()
+        ws = torch.empty(L.nerf_mlp_dw_workspace_bytes(dt, M), dtype=torch.uint8, device=dev)
+        b["grad"].zero_()
+        assert L.nerf_mlp_bwd_dw_ws(dt, M, ptr(b["act"]), ptr(b["dz"]), ptr(b["grad"]), ptr(ws), s) == 0
+    torch.cuda.synchronize()
+    for name, _ in libs[1:]:
+        out["identical_to_" + n0][name]["grad_deterministic"] = bool(torch.equal(bufs[name]["grad"],
+                                                                                 bufs[n0]["grad"]))
     for name, _ in libs:
         out[name] = {k: round(statistics.median(times[(name, k)]), 4) for k in ("fwd", "fwd_train", "dx", "dw")}
     print(json.dumps(out), flush=True)
