@@ -20,6 +20,7 @@
 #include "common.h"
 #include "mlp_tables.h"
 
+#include <mutex>
 #include <utility>
 
 namespace nerf {
@@ -334,10 +335,11 @@ constexpr UnitOffsets unit_offsets() {
 }
 
 // one thread per 16-B lane slot of one chunk
-template <class P, int DIR>
-__global__ void pack_kernel(ParamPtrs prm, UnitOffsets uo, char* out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total_chunks(P::CH, DIR) * 64) return;
+// The sources of packed lane-chunk i (chunk i >> 6, lane i & 63): weight(e, wp, idx, c) for each of its
+// E elements (wp = -1: a zero element; else element idx of parameter wp, split part c of P::cvt_c), or, on
+// a forward unit's bias chunk, bias(e, wp, idx) for its 4 fp32 values.
+template <class P, int DIR, class Weight, class Bias>
+__device__ __forceinline__ void pack_sources(int64_t i, const UnitOffsets& uo, Weight&& weight, Bias&& bias) {
   const int lane = (int)(i & 63);
   const int chunk = (int)(i >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -345,41 +347,113 @@ __global__ void pack_kernel(ParamPtrs prm, UnitOffsets uo, char* out) {
   int u = 0;
   for (int k = 1; k < nunit; ++k) u += uo.off[k] <= chunk ? 1 : 0;
   const int within = chunk - uo.off[u];
-  char* dst = out + i * 16;
   if (DIR == 0 && within == fwd_unit_tiles(u) * P::CH) {
     // bias chunk: lanes 0..7 hold the 32 biases of the unit's output rows, rest zero
     const int L = fwd_unit_layer(u), n = u - fwd_unit_first(L);
     const int wp = fwd_out_weight(L, n);
-    float* d = (float*)dst;
     for (int e = 0; e < 4; ++e) {
       const int row = lane * 4 + e;
-      d[e] = (lane < 8 && row < fwd_out_valid(L, n)) ? prm.p[wp + 1][fwd_out_row0(L, n) + row] : 0.f;
+      const bool ok = lane < 8 && row < fwd_out_valid(L, n);
+      bias(e, ok ? wp + 1 : -1, (int64_t)(fwd_out_row0(L, n) + row));
     }
     return;
   }
   const int t = within / P::CH, c = within % P::CH;
-  typename P::Store vals[P::E];
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const int rho = P::rho_of(c, e);
     const int ar = acc_row(rho, h);
-    float v = 0.f;
+    int wp = -1;
+    int64_t idx = 0;
     if (DIR == 0) {
       const int L = fwd_unit_layer(u), n = u - fwd_unit_first(L);
-      const int wp = fwd_out_weight(L, n);
+      const int w = fwd_out_weight(L, n);
       const int row = fwd_out_row0(L, n) + r, col = fwd_in_colbase(L, t) + ar;
-      if (r < fwd_out_valid(L, n) && ar < fwd_in_valid(L, t)) v = prm.p[wp][(int64_t)row * weight_K(wp) + col];
+      if (r < fwd_out_valid(L, n) && ar < fwd_in_valid(L, t)) wp = w, idx = (int64_t)row * weight_K(w) + col;
     } else {
       // A[i = forward in-feature (r)][p = forward out-feature of forward tile t (ar)]
       const int s = bwd_unit_stage(u), j = u - bwd_unit_first(s), L = bwd_fwd_layer(s);
-      const int wp = fwd_out_weight(L, t);
+      const int w = fwd_out_weight(L, t);
       const int row = fwd_out_row0(L, t) + ar, col = bwd_out_colbase(s, j) + r;
-      if (ar < fwd_out_valid(L, t)) v = prm.p[wp][(int64_t)row * weight_K(wp) + col];
+      if (ar < fwd_out_valid(L, t)) wp = w, idx = (int64_t)row * weight_K(w) + col;
     }
-    vals[e] = P::cvt_c(v, c);
+    weight(e, wp, idx, c);
   }
+}
+
+// direct pack (any parameter layout): one thread per lane-chunk, the sources walked on the device
+template <class P, int DIR>
+__global__ void pack_kernel(ParamPtrs prm, UnitOffsets uo, char* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total_chunks(P::CH, DIR) * 64) return;
+  char* dst = out + i * 16;
+  typename P::Store vals[P::E];
+  bool is_bias = false;
+  pack_sources<P, DIR>(
+      i, uo,
+      [&](int e, int wp, int64_t idx, int c) { vals[e] = P::cvt_c(wp < 0 ? 0.f : prm.p[wp][idx], c); },
+      [&](int e, int wp, int64_t idx) {
+        is_bias = true;
+        ((float*)dst)[e] = wp < 0 ? 0.f : prm.p[wp][idx];
+      });
+  if (is_bias) return;
 #pragma unroll
   for (int e = 0; e < P::E; ++e) ((typename P::Store*)dst)[e] = vals[e];
+}
+
+// Pack plan (r5): the sources of every packed element, built once per (policy, direction, device) by
+// pack_plan_kernel, so that the per-step repack of a net whose 24 parameters lie back to back (FusedAdam's
+// flat buffer) is one gather (pack_gather_kernel: ~30 instructions per lane-chunk instead of the ~2,000 of
+// the unit / layer walk above, bit-identical).  Entry: bits 0-23 the element's offset in the net's flat
+// parameters, bits 24-26 the split part c; PLAN_ZERO a zero element; PLAN_BIAS in entry E - 1 marks a
+// bias lane-chunk whose entries 0-3 are fp32 values (E = 8 policies; fp32's E = 4 stores floats anyway).
+constexpr uint32_t PLAN_ZERO = 0xFFFFFFFFu;
+constexpr uint32_t PLAN_BIAS = 0xFE000000u;
+template <class P, int DIR>
+__global__ void pack_plan_kernel(UnitOffsets uo, uint32_t* plan) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total_chunks(P::CH, DIR) * 64) return;
+  uint32_t* pl = plan + i * P::E;
+  auto code = [](int wp, int64_t idx, int c) {
+    return wp < 0 ? PLAN_ZERO : (uint32_t)(param_offset(wp) + idx) | ((uint32_t)c << 24);
+  };
+  bool is_bias = false;
+  uint32_t ent[P::E];
+  pack_sources<P, DIR>(
+      i, uo, [&](int e, int wp, int64_t idx, int c) { ent[e] = code(wp, idx, c); },
+      [&](int e, int wp, int64_t idx) {
+        is_bias = true;
+        ent[e] = code(wp, idx, 0);
+      });
+  if (is_bias)
+    for (int e = 4; e < P::E; ++e) ent[e] = e == P::E - 1 ? PLAN_BIAS : PLAN_ZERO;
+  for (int e = 0; e < P::E; ++e) pl[e] = ent[e];
+}
+template <class P>
+__global__ void pack_gather_kernel(const float* __restrict__ flat, const uint32_t* __restrict__ plan, char* out,
+                                   int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t ent[P::E];
+#pragma unroll
+  for (int q = 0; q < P::E / 4; ++q) {
+    const uint4 v = ((const uint4*)(plan + i * P::E))[q];
+    ent[4 * q] = v.x, ent[4 * q + 1] = v.y, ent[4 * q + 2] = v.z, ent[4 * q + 3] = v.w;
+  }
+  char* dst = out + i * 16;
+  if (P::E == 8 && ent[P::E - 1] == PLAN_BIAS) {
+    float f[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[e] = ent[e] == PLAN_ZERO ? 0.f : flat[ent[e] & 0xFFFFFFu];
+    *(float4*)dst = make_float4(f[0], f[1], f[2], f[3]);
+    return;
+  }
+  typename P::Store vals[P::E];
+#pragma unroll
+  for (int e = 0; e < P::E; ++e)
+    vals[e] = P::cvt_c(ent[e] == PLAN_ZERO ? 0.f : flat[ent[e] & 0xFFFFFFu], (int)((ent[e] >> 24) & 7u));
+  static_assert(sizeof(vals) == 16, "a lane-chunk is 16 bytes");
+  *(uint4*)dst = __builtin_bit_cast(uint4, vals);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2143,10 +2217,46 @@ static void launch_fwd_any(const FwdArgs& a, bool store, bool density, hipStream
 // unit (no NERF_MLP_PREC) only declares them, so the three precisions compile in parallel.
 namespace nerf {
 namespace mlp {
+// the pack plan of (P, dir) on the current device: built on first use (one launch, then a stream sync),
+// kept for the process; null if it cannot be allocated (the caller falls back to pack_kernel)
+template <class P>
+static const uint32_t* pack_plan(int dir, hipStream_t stream) {
+  static std::mutex mu;
+  static uint32_t* plans[64][2] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  uint32_t*& plan = plans[dev][dir];
+  if (!plan) {
+    const int64_t n = total_chunks(P::CH, dir) * 64;
+    uint32_t* p = nullptr;
+    if (hipMalloc(&p, (size_t)n * P::E * sizeof(uint32_t)) != hipSuccess) return nullptr;
+    dim3 grid((unsigned)((n + 255) / 256));
+    if (dir == 0) hipLaunchKernelGGL((pack_plan_kernel<P, 0>), grid, dim3(256), 0, stream, unit_offsets<P::CH, 0>(), p);
+    else hipLaunchKernelGGL((pack_plan_kernel<P, 1>), grid, dim3(256), 0, stream, unit_offsets<P::CH, 1>(), p);
+    if (hipStreamSynchronize(stream) != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    plan = p;
+  }
+  return plan;
+}
 template <class P>
 void mlp_pack_impl(const ParamPtrs& prm, int dir, char* dst, hipStream_t stream) {
   const int64_t n = total_chunks(P::CH, dir) * 64;
   dim3 grid((unsigned)((n + 255) / 256));
+  // the 24 parameters back to back (FusedAdam's flat buffer): the plan gather (NERF_PACK_PLAN=0: always
+  // the direct pack, for A/B timing)
+  const char* env = getenv("NERF_PACK_PLAN");
+  bool flat = !(env && env[0] == '0');
+  for (int k = 1; k < NPARAM; ++k) flat = flat && prm.p[k] == prm.p[0] + param_offset(k);
+  if (flat) {
+    if (const uint32_t* plan = pack_plan<P>(dir, stream)) {
+      hipLaunchKernelGGL((pack_gather_kernel<P>), grid, dim3(256), 0, stream, prm.p[0], plan, dst, n);
+      return;
+    }
+  }
   if (dir == 0) hipLaunchKernelGGL((pack_kernel<P, 0>), grid, dim3(256), 0, stream, prm, unit_offsets<P::CH, 0>(), dst);
   else hipLaunchKernelGGL((pack_kernel<P, 1>), grid, dim3(256), 0, stream, prm, unit_offsets<P::CH, 1>(), dst);
 }

@@ -720,6 +720,38 @@ def test_image_metrics_match_host_evaluator(cuda, ops, H, W, noise):
     assert abs(ssim - ref_ssim) < 1e-9, (ssim, ref_ssim)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3", "bf16x3f", "bf16x6"])
+def test_pack_plan_gather_matches_direct_pack(cuda, ops, seeded_state, dtype):
+    """nerf_mlp_pack gathers through its cached pack plan when the 24 parameters lie back to back
+    (FusedAdam's flat buffer) and walks the units directly otherwise: byte-identical packs, both
+    directions (csrc/mlp.hip pack_plan_kernel / pack_gather_kernel / pack_kernel)."""
+    import ctypes
+    from nerf_amd._lib import check, lib, ptr, stream_of
+    L = lib()
+    params = [seeded_state[f"model.{n}"].to(cuda) for n in ops.NET_PARAM_NAMES]
+    offs = [L.nerf_mlp_param_offset(i) for i in range(24)]
+    flat = torch.cat([p.reshape(-1) for p in params])
+    assert offs == [sum(p.numel() for p in params[:i]) for i in range(24)]
+    views = [flat[o:o + p.numel()] for o, p in zip(offs, params)]
+    gapped = torch.zeros(flat.numel() + 16 * 24, device=cuda)   # the same values, 16 floats apart
+    sep = []
+    for i, p in enumerate(params):
+        v = gapped[offs[i] + 16 * i:offs[i] + 16 * i + p.numel()]
+        v.copy_(p.reshape(-1))
+        sep.append(v)
+    code = ops.dtype_code(dtype)
+    for d in ((0,) if dtype == "bf16x6" else (0, 1)):
+        outs = []
+        for ps in (views, sep):
+            arr = ctypes.cast((ctypes.c_void_p * 24)(*[p.data_ptr() for p in ps]), ctypes.c_void_p)
+            buf = torch.full((L.nerf_mlp_packed_bytes(code, d),), 0xAB, dtype=torch.uint8, device=cuda)
+            check(L.nerf_mlp_pack(arr, code, ptr(buf if d == 0 else None), ptr(buf if d == 1 else None),
+                                  stream_of(flat)), "pack")
+            outs.append(buf)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), (dtype, d)
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16", "bf16x3f"])
 def test_mlp_dw_deterministic(cuda, ops, seeded_state, dtype):
     """dW with the workspace (per-item partials, fixed-order reduce) is bit-identical run to

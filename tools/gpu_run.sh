@@ -14,6 +14,7 @@
 #   mlp=ARGS         tools/mlp_bench.py ARGS (comma-free; use + for spaces)
 #   march=DTYPE      tools/march_bench.py --dtype DTYPE
 #   ab=DTYPE         tools/step_ab.py --dtype DTYPE (whole-step A/B of the backward scheduling knobs)
+#   abp=DTYPE        tools/step_ab.py --dtype DTYPE --configs one,noplan (the pack plan gather vs the direct repack)
 #   abe=DTYPE        tools/step_ab.py --dtype DTYPE --configs one,events (cost of the per-kernel timing events)
 #   abu=DTYPE        tools/step_ab.py --dtype DTYPE --configs one,unfused (the round-4 fused launches split again)
 #   traffic=DTYPE    PMC FETCH_SIZE / WRITE_SIZE passes of a short bench -> gpurun_out/traffic_DTYPE.json
@@ -58,6 +59,7 @@ for step in "$@"; do
     abe=*) run "abe_${step#abe=}" 600 python3 -u tools/step_ab.py --dtype "${step#abe=}" --configs one,events --rounds 7 ;;
     abu=*) run "abu_${step#abu=}" 600 python3 -u tools/step_ab.py --dtype "${step#abu=}" --configs one,unfused --rounds 7 ;;
     ab=*) run "ab_${step#ab=}" 600 python3 -u tools/step_ab.py --dtype "${step#ab=}" ;;
+    abp=*) run "abp_${step#abp=}" 600 python3 -u tools/step_ab.py --dtype "${step#abp=}" --configs one,noplan --rounds 7 ;;
     march=*) run "march_${step#march=}" 400 python3 tools/march_bench.py --dtype "${step#march=}" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -11,6 +11,8 @@ Configurations (ops.BWD_CHUNK x ops.DW_STREAM):
   chunk+stream
   unfused  one, with the round-4 fused launches split again (composite + sample_pdf, the MSE pair)
   events   one, with bench.py's per-kernel HIP timing events recorded (ops.KERNEL_TIMES)
+  noplan   one, with the weight repack walking the units on the device (NERF_PACK_PLAN=0) instead of
+           gathering through the cached pack plan
 Prints one JSON line: median ms/step per configuration.
 """
 import argparse
@@ -53,6 +55,7 @@ def main():
         # "events": bench.py's per-launch HIP timing events (ops.kernel_timer) recorded around every kernel
         ops.KERNEL_TIMES.reset()
         ops.KERNEL_TIMES.enabled = "events" in c
+        os.environ["NERF_PACK_PLAN"] = "0" if "noplan" in c else "1"
 
     times = {c: [] for c in configs}
     for r in range(a.rounds + 1):
