@@ -721,6 +721,25 @@ def test_image_metrics_match_host_evaluator(cuda, ops, H, W, noise):
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3", "bf16x3f", "bf16x6"])
+def test_mlp_ragged_sizes_row_independent(cuda, ops, seeded_state, dtype):
+    """Ragged launch sizes (1, 31, 32, 33, 255, 257, 4133 samples: partial 32-sample wave blocks and
+    256-sample workgroups): every sample's raw output is its row of the 4,133-sample launch, bit for bit
+    (the MLP is row-independent; padding rows never leak into real ones)."""
+    g = torch.Generator().manual_seed(29)
+    big = 4133
+    pts = (torch.rand(big, 3, generator=g) * 3 - 1.5).to(cuda)
+    ndir = 97
+    vd = torch.nn.functional.normalize(torch.randn(ndir, 3, generator=g), dim=-1).to(cuda)
+    di = torch.randint(0, ndir, (big,), generator=g, dtype=torch.int32).to(cuda)
+    packer = ops.PackedMLP([seeded_state[f"model.{n}"].to(cuda) for n in ops.NET_PARAM_NAMES])
+    with torch.no_grad():
+        ref = ops.mlp(packer, pts, vd, 1, di, dtype)
+        for m in (1, 31, 32, 33, 255, 257):
+            got = ops.mlp(packer, pts[:m].contiguous(), vd, 1, di[:m].contiguous(), dtype)
+            assert torch.equal(got, ref[:m]), (dtype, m)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3", "bf16x3f", "bf16x6"])
 def test_pack_plan_gather_matches_direct_pack(cuda, ops, seeded_state, dtype):
     """nerf_mlp_pack gathers through its cached pack plan when the 24 parameters lie back to back
     (FusedAdam's flat buffer) and walks the units directly otherwise: byte-identical packs, both
