@@ -689,6 +689,10 @@ __host__ __device__ constexpr bool finished_in_group(int g, int u) {
 // training forward had 70 % of its non-MFMA instructions in 138 runs of > 20 between two
 // MFMAs).  With NP parts, part p (register pairs [8p/NP, 8(p+1)/NP)) is issued FINISH_DELAY + p
 // steps into the next unit, clamped to that unit's last step; the last part stores.
+// (Only the defaults below are verified: run-to-run identical stores, tests/test_gpu_kernels.py
+// test_training_kernels_bitwise_deterministic.  Measured in r5, NERF_FINISH_PARTS_BF16 = 2 / 8 wrote masks / dz
+// that differed between two runs of the same launch although the static hand-off check passed -- a placement-
+// dependent LDS hazard; tools/mlp_bench.py --libs A,A-copy reports it as identical_to_... false.)
 #ifndef NERF_FINISH_PARTS_F32
 #define NERF_FINISH_PARTS_F32 1  // (fp32: 8 parts + spread DMA measured 4.88 -> 5.05 ms, training forward)
 #endif

@@ -720,6 +720,40 @@ def test_image_metrics_match_host_evaluator(cuda, ops, H, W, noise):
     assert abs(ssim - ref_ssim) < 1e-9, (ssim, ref_ssim)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3", "bf16x3f"])
+def test_training_kernels_bitwise_deterministic(cuda, ops, seeded_state, dtype):
+    """The training forward, dX and deterministic dW run twice on the same inputs write the same bytes: raw,
+    activation / mask / dz stores and the gradient.  The weight ring's hand-offs are counted waits and
+    barriers the compiler cannot see (csrc/mlp.hip); a late LDS read or an early DMA would show here as
+    run-to-run differences (r5: non-default finish-part placements did, NERF_FINISH_PARTS_BF16=2 / 8)."""
+    from nerf_amd._lib import check, lib, ptr, stream_of
+    L = lib()
+    g = torch.Generator().manual_seed(31)
+    M = 131101
+    code = ops.dtype_code(dtype)
+    packer = ops.PackedMLP([seeded_state[f"model.{n}"].to(cuda).contiguous() for n in ops.NET_PARAM_NAMES])
+    pts = (torch.rand(M, 3, generator=g) * 3 - 1.5).to(cuda)
+    vd = torch.nn.functional.normalize(torch.randn(M // 9 + 1, 3, generator=g), dim=-1).to(cuda)
+    d_raw = (torch.randn(M, 4, generator=g) * 1e-2).to(cuda)
+    s = stream_of(pts)
+    outs = []
+    for _ in range(2):
+        b = dict(raw=torch.zeros(M, 4, device=cuda),
+                 act=torch.zeros(L.nerf_mlp_act_bytes(code, M), dtype=torch.uint8, device=cuda),
+                 masks=torch.zeros(L.nerf_mlp_mask_bytes(M), dtype=torch.uint8, device=cuda),
+                 dz=torch.zeros(L.nerf_mlp_dz_bytes(code, M), dtype=torch.uint8, device=cuda),
+                 grad=torch.zeros(L.nerf_mlp_net_params(), device=cuda))
+        ws = torch.empty(L.nerf_mlp_dw_workspace_bytes(code, M), dtype=torch.uint8, device=cuda)
+        check(L.nerf_mlp_fwd(ptr(packer.get(code, 0)), code, ptr(pts), ptr(vd), 9, None, M, 1, ptr(b["raw"]),
+                             ptr(b["act"]), ptr(b["masks"]), s), "fwd")
+        check(L.nerf_mlp_bwd_dx(ptr(packer.get(code, 1)), code, ptr(d_raw), M, ptr(b["masks"]), ptr(b["dz"]), s), "dx")
+        check(L.nerf_mlp_bwd_dw_ws(code, M, ptr(b["act"]), ptr(b["dz"]), ptr(b["grad"]), ptr(ws), s), "dw")
+        outs.append(b)
+    torch.cuda.synchronize()
+    for k in ("raw", "act", "masks", "dz", "grad"):
+        assert torch.equal(outs[0][k], outs[1][k]), (dtype, k)
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3", "bf16x3f", "bf16x6"])
 def test_mlp_ragged_sizes_row_independent(cuda, ops, seeded_state, dtype):
     """Ragged launch sizes (1, 31, 32, 33, 255, 257, 4133 samples: partial 32-sample wave blocks and
