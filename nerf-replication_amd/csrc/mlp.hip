@@ -295,13 +295,23 @@ typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
 __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t d) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2, d), (i16x2){0, 0}));
 }
-// 1 in each half that is non-zero (v_pk_min_u16 with 1)
-// (asm: written with __builtin_elementwise_min, hipcc expands it into ~8 compares and selects
-// per pair once it knows the halves come from a ReLU'd conversion)
-__device__ __forceinline__ uint32_t nonzero_bf16x2(uint32_t d) {
-  uint32_t r;
-  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(d), "s"(0x00010001u));
-  return r;
+// 1 in each half that is non-zero: v_pk_min_u16 with `one` = 0x00010001, which the caller holds in an
+// SGPR laundered through an empty asm (no instruction) -- hipcc then emits the one v_pk_min_u16 itself;
+// knowing the operand is 1 it rewrites min(x, 1) into a compare and a select per half.
+// Round 6: this WAS an inline-asm v_pk_min_u16.  hipcc's hazard recognizer does not model the MFMA
+// hazards of an inline-asm VGPR write: with finish parts 2 it allocated the asm's output to v1, a dead
+// lane of the rgb unit's accumulator v[0:15] whose MFMA had issued one instruction earlier and still
+// had its write of v[0:15] pending -- the MFMA's late write-back replaced the mask bits on some runs
+// (the round-5 "masks differ run to run" finding; tools/mfma_war_scan.py: asm write 1 wait state after
+// the MFMA, against >= 13 for every compiler-placed write).  No VGPR-writing inline asm is left in the
+// MFMA kernels (tools/asm_check.py fails one).
+__device__ __forceinline__ uint32_t nonzero_bf16x2(uint32_t d, uint32_t one) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, d), __builtin_bit_cast(u16x2, one)));
+}
+__device__ __forceinline__ uint32_t opaque_one16() {
+  uint32_t one = 0x00010001u;
+  asm("" : "+s"(one));
+  return one;
 }
 
 template <class P> __host__ __device__ constexpr int samples_per_block() { return P::WAVES * 32; }
@@ -689,10 +699,12 @@ __host__ __device__ constexpr bool finished_in_group(int g, int u) {
 // training forward had 70 % of its non-MFMA instructions in 138 runs of > 20 between two
 // MFMAs).  With NP parts, part p (register pairs [8p/NP, 8(p+1)/NP)) is issued FINISH_DELAY + p
 // steps into the next unit, clamped to that unit's last step; the last part stores.
-// (Only the defaults below are verified: run-to-run identical stores, tests/test_gpu_kernels.py
-// test_training_kernels_bitwise_deterministic.  Measured in r5, NERF_FINISH_PARTS_BF16 = 2 / 8 wrote masks / dz
-// that differed between two runs of the same launch although the static hand-off check passed -- a placement-
-// dependent LDS hazard; tools/mlp_bench.py --libs A,A-copy reports it as identical_to_... false.)
+// Any value is checked at compile time: FinishSchedule (below) static_asserts that no MFMA reads a tile pair
+// before the part that writes it.  (Round 5 saw NERF_FINISH_PARTS_BF16 = 2 / 8 write masks / dZ that differed
+// run to run.  Parts 8 is that clamping hazard and no longer compiles; parts 2 was an inline-asm VGPR write
+// racing an MFMA write-back (nonzero_bf16x2), fixed for every placement.  Round 6, tools/race_diag.py,
+// profiles/r6/race_diag_*.json: bf16 parts 2 / 4 and bf16x3 parts 4 / 8 bit-identical, run to run and to
+// each other.)
 #ifndef NERF_FINISH_PARTS_F32
 #define NERF_FINISH_PARTS_F32 1  // (fp32: 8 parts + spread DMA measured 4.88 -> 5.05 ms, training forward)
 #endif
@@ -759,6 +771,174 @@ __host__ __device__ constexpr int handoff_vmcnt_spread(int g, StoresFn unit_stor
     if (s >= last) n += unit_stores(u);
   }
   return n;
+}
+
+// ------------------------------------------------------------------------------------
+// Register tile slots and the finish-schedule check (r6).
+//
+// A wave's B-operand tiles live in registers: the activation / gradient ping-pong arrays Ha[0..7]
+// and Hb[0..7], the encodings X[0..1] and D (forward) and the output-gradient seeds G and DA (dX).
+// Every unit reads its input tiles from slots and its finish parts write its output tile, pair by
+// pair, IN PLACE into a slot -- which the next layer's first unit reads.  The two tables below
+// are the kernels' own (FwdWave::in_tile / DxWave::in_tile and the finishes go through them), so
+// the schedule model below checks the code that runs.
+//
+// The race found in round 5 (bf16 finish parts 2 / 8: masks / dZ that differed between two runs
+// of one launch) is this hand-off.  A finish part is issued FINISH_DELAY + p steps into the next
+// unit, CLAMPED to that unit's last step, and within a step the finish runs after the MFMA.
+// Where the next unit has few input tiles -- LRGB after LV (4 tiles), the dX stage bV after
+// bRGB (4 tiles) -- eight parts land at steps 3..7 of an 8-step unit, and the parts writing
+// pairs 3..7 of tile 3 come after the MFMAs that read them (steps 6 and 7).  Those MFMAs read the
+// slot's OLD registers: in the forward the previous layer's values (deterministic, wrong), in the
+// dX chain Hb[3] before its first write (uninitialised registers: different on every run).  The
+// ISA-level hand-off check could not see it: it is a register dependence the program order
+// itself gets wrong, not a memory-counter one.  finish_schedule_ok() below simulates every
+// group's steps and fails the build of any placement where an MFMA reads a pair before its
+// producer's part (or a later producer's part overwrites it first), or a part reads `pend` after
+// it was reassigned.
+// ------------------------------------------------------------------------------------
+enum TileSlot { TS_HA = 0, TS_HB = 8, TS_X = 16, TS_D = 18, TS_G = 19, TS_DA = 20, TS_NONE = -1 };
+__host__ __device__ constexpr bool finish_slot(int s) { return s >= TS_HA && s < TS_X; }  // written by finishes
+// forward layer L: input tile t, output tile n
+__host__ __device__ constexpr int fwd_in_slot(int L, int t) {
+  return L == L0 ? TS_X + t
+       : L == L5 ? (t < 2 ? TS_X + t : TS_HA + t - 2)
+       : L == LV ? (t < 8 ? TS_HA + t : (int)TS_D)
+       : L == LRGB ? TS_HB + t
+       : (L == L1 || L == L3 || L == L7) ? TS_HA + t
+       : TS_HB + t;  // L2, L4, L6, LFA
+}
+__host__ __device__ constexpr int fwd_out_slot(int L, int n) {
+  return L == LRGB || (L == LFA && n == 8) ? (int)TS_NONE  // (rgb / alpha: scalars)
+       : (L == L0 || L == L2 || L == L4 || L == L6 || L == LFA) ? TS_HA + n
+       : TS_HB + n;  // L1, L3, L5, L7, LV
+}
+// dX stage s: input tile t, output tile j
+__host__ __device__ constexpr int bwd_in_slot(int s, int t) {
+  return s == B_RGB ? (int)TS_G
+       : s == B_V ? TS_HB + t
+       : s == B_FA ? (t < 8 ? TS_HA + t : (int)TS_DA)
+       : (s == B_7 || s == B_5 || s == B_3 || s == B_1) ? TS_HB + t
+       : TS_HA + t;  // B_6, B_4, B_2
+}
+__host__ __device__ constexpr int bwd_out_slot(int s, int j) {
+  return (s == B_RGB || s == B_FA || s == B_6 || s == B_4 || s == B_2) ? TS_HB + j : TS_HA + j;
+}
+template <int DIR> __host__ __device__ constexpr int unit_in_slot(int u, int t) {
+  return DIR == 0 ? fwd_in_slot(fwd_unit_layer(u), t) : bwd_in_slot(bwd_unit_stage(u), t);
+}
+template <int DIR> __host__ __device__ constexpr int unit_out_slot(int u) {
+  return DIR == 0 ? fwd_out_slot(fwd_unit_layer(u), u - fwd_unit_first(fwd_unit_layer(u)))
+                  : bwd_out_slot(bwd_unit_stage(u), u - bwd_unit_first(bwd_unit_stage(u)));
+}
+// register pairs (bit k = registers 2k, 2k + 1) of a tile that MFMA chunk c reads / finish part p writes
+template <class P> __host__ __device__ constexpr int chunk_pairs(int c) {
+  int m = 0;
+  for (int e = 0; e < P::E; ++e) {
+    const int rho = P::rho_of(c, e);
+    if (rho < 16) m |= 1 << (rho >> 1);
+  }
+  return m;
+}
+template <class P> __host__ __device__ constexpr int part_pairs(int p) {
+  constexpr int NP = finish_parts<P>();
+  int m = 0;
+  for (int k = 8 * p / NP; k < 8 * (p + 1) / NP; ++k) m |= 1 << k;
+  return m;
+}
+// Positions in the straight-line schedule: 4 * (global step) + phase, the phases of one step in
+// group_body's order: 0 DMA pieces, 1 pend / init + MFMA, 2 the previous unit's finish parts, 3 the
+// group's last unit (finished in-group, or parked in `pend` for the next group).
+// finish_schedule_violation() is 0 when the schedule is sound; else a code naming the first
+// violation: 1 an MFMA reads a pair before its producer's part writes it (or reads a slot no unit
+// wrote), 2 a later producer's part overwrites the pair before the read, 3 a part reads `pend`
+// after it was reassigned, 4 a finish part is never issued.
+template <class P, int DIR, bool DENSITY>
+struct FinishSchedule {
+  static constexpr int NU = DIR == 0 ? NUNIT_FWD : NUNIT_BWD;
+  static constexpr int NP = finish_parts<P>();
+  int pos[NUNIT_FWD > NUNIT_BWD ? NUNIT_FWD : NUNIT_BWD][8];   // position of part p of unit u (-1: none)
+  int pend_at[NUNIT_FWD > NUNIT_BWD ? NUNIT_FWD : NUNIT_BWD];  // position at which `pend` takes unit u (-1)
+  int violation;
+  __host__ __device__ constexpr FinishSchedule() : pos(), pend_at(), violation(0) {
+    const auto& T = GroupTable<DIR, DENSITY, P::CH>::t;
+    for (int u = 0; u < NU; ++u) {
+      pend_at[u] = -1;
+      for (int p = 0; p < 8; ++p) pos[u][p] = -1;
+    }
+    int base = 0;
+    for (int g = 0; g < T.n; ++g) {
+      const Group G = T.g[g];
+      const int NS = group_steps<DIR, DENSITY, P::CH>(g);
+      const int last = G.u0 + G.n - 1;
+      // units finished in g: the previous group's last unit (cross-group finish) and G's own
+      for (int u = (g > 0 ? T.g[g - 1].u0 + T.g[g - 1].n - 1 : G.u0); u <= last; ++u)
+        for (int p = 0; p < NP; ++p) {
+          const int st = part_step<P, DIR, DENSITY>(g, u, p);
+          if (st >= 0) pos[u][p] = 4 * (base + st) + (u == last ? 3 : 2);
+        }
+      for (int j = 1, k = unit_tiles<DIR>(G.u0) * P::CH; j < G.n; k += unit_tiles<DIR>(G.u0 + j) * P::CH, ++j)
+        pend_at[G.u0 + j - 1] = 4 * (base + k) + 1;  // (the first step of unit j)
+      if (!finished_in_group<DIR, DENSITY, P::CH, cross_finish<P, DIR>()>(g, last)) pend_at[last] = 4 * (base + NS - 1) + 3;
+      base += NS;
+    }
+    violation = check();
+  }
+  __host__ __device__ constexpr int check() const {
+    const auto& T = GroupTable<DIR, DENSITY, P::CH>::t;
+    int out[NUNIT_FWD > NUNIT_BWD ? NUNIT_FWD : NUNIT_BWD] = {}, next[NUNIT_FWD > NUNIT_BWD ? NUNIT_FWD : NUNIT_BWD] = {};
+    for (int u = 0; u < NU; ++u) {
+      out[u] = unit_used<DIR, DENSITY>(u) ? unit_out_slot<DIR>(u) : (int)TS_NONE;
+      next[u] = -1;
+    }
+    for (int u = NU - 1; u >= 0; --u)  // next unit writing the same slot
+      for (int v = u + 1; v < NU && next[u] < 0; ++v)
+        if (finish_slot(out[u]) && out[v] == out[u]) next[u] = v;
+    for (int u = 0; u < NU; ++u) {
+      if (!unit_used<DIR, DENSITY>(u)) continue;
+      for (int p = 0; p < NP; ++p) {
+        if (pos[u][p] < 0) return 4;
+        if ((pos[u][p] & 3) == 3) continue;  // finished in-group from `acc`
+        // `pend` holds u from pend_at[u] until the next unit's assignment
+        if (pend_at[u] < 0 || pend_at[u] >= pos[u][p]) return 3;
+        for (int v = u + 1; v < NU; ++v)
+          if (pend_at[v] >= 0 && pend_at[v] < pos[u][p]) return 3;
+      }
+    }
+    int writer[TS_X] = {};  // last unit (in unit order, before the reading unit) whose output is the slot
+    for (int s = 0; s < TS_X; ++s) writer[s] = -1;
+    int base = 0;
+    for (int g = 0; g < T.n; ++g) {
+      const Group G = T.g[g];
+      for (int j = 0; j < G.n; ++j) {
+        const int u = G.u0 + j;
+        for (int v = (j == 0 ? 0 : u - 1); v < u; ++v)
+          if (finish_slot(out[v])) writer[out[v]] = v;
+        const int nt = unit_tiles<DIR>(u);
+        for (int t = 0; t < nt; ++t) {
+          const int slot = unit_in_slot<DIR>(u, t);
+          if (!finish_slot(slot)) {
+            base += P::CH;
+            continue;
+          }
+          const int prod = writer[slot];
+          if (prod < 0) return 1;
+          for (int c = 0; c < P::CH; ++c, ++base) {
+            const int rpos = 4 * base + 1, cp = chunk_pairs<P>(c);
+            for (int p = 0; p < NP; ++p) {
+              if (!(part_pairs<P>(p) & cp)) continue;
+              if (pos[prod][p] >= rpos) return 1;
+              if (next[prod] >= 0 && pos[next[prod]][p] >= 0 && pos[next[prod]][p] < rpos) return 2;
+            }
+          }
+        }
+      }
+    }
+    return 0;
+  }
+};
+template <class P, int DIR, bool DENSITY> __host__ __device__ constexpr int finish_schedule_violation() {
+  return FinishSchedule<P, DIR, DENSITY>{}.violation;
 }
 
 // W: the wave object; it provides in_tile<u, t>(), prefetch<u>() (issue unit u's side
@@ -832,16 +1012,22 @@ __device__ __forceinline__ void fetch_piece(const uint4* gsrc, uint32_t slot_bas
   glds16_asm(gsrc + (int64_t)(C0 + k) * 64 + lane, slot_base + (uint32_t)k * 1024u);
 }
 
-// Lean form of the same piece (NERF_DMA_LEAN): 3 instructions instead of 7.  Wave w's piece I is
-// chunk w + WAVES I, so with the per-lane VGPR vlane = 16 lane + 1024 w and the wave-uniform
-// swave = LDS base + 1024 w held for the whole kernel, the piece's global offset and LDS address
-// are those plus compile-time constants: `s_add_u32 m0` (the LDS destination), `v_add_u32` (the
-// per-lane offset, SADDR form on the packed-weight base; it is also the wait state the m0 write
-// needs before the DMA) and the DMA.  M0 is not saved: no compiler code of these kernels touches
-// it (tools/asm_check.py checks the emitted code).  s_add_u32 writes SCC: declared clobbered (without
-// it hipcc kept a comparison in SCC across the statement and the last group's surplus-wave
-// selection went wrong -- the rgb bias chunk was never copied).  A surplus wave of the last piece
-// (w + WAVES I > NCH - 1) re-copies its previous piece instead: the same bytes to the same place.
+// Lean form of the same piece (NERF_DMA_LEAN).  Wave w's piece I is chunk w + WAVES I, so with the
+// per-lane VGPR vlane = 16 lane + 1024 w and the wave-uniform swave = LDS base + 1024 w held for the
+// whole kernel, the piece's global offset and LDS address are those plus compile-time constants:
+// `s_add_u32 m0` (the LDS destination), `s_nop 0` (the wait state an M0 write needs before an
+// LDS-DMA) and the DMA in the SADDR form on the packed-weight base; the per-lane offset vlane + GOFF is
+// a v_add_u32 that hipcc places itself (4 instructions per piece; round 5 put the v_add_u32 inside
+// the asm, as the m0 wait state, for 3).  Round 6: no VGPR is written inside inline asm any more --
+// hipcc's hazard recognizer does not cover an asm VGPR write that lands on a register an in-flight
+// MFMA still writes or reads as SrcC (the mask race, nonzero_bf16x2 above); a compiler-placed
+// v_add_u32 gets its wait states.  M0 is not saved: no compiler code of these kernels touches it
+// (tools/asm_check.py checks the emitted code; M0 is a reserved register, so clang ignores it in a
+// clobber list -- "-Winline-asm: reserved registers on the clobber list may not be preserved").  s_add_u32 writes SCC: declared
+// clobbered too (without it hipcc kept a comparison in SCC across the statement and the last group's
+// surplus-wave selection went wrong -- the rgb bias chunk was never copied).  A surplus wave of the
+// last piece (w + WAVES I > NCH - 1) re-copies its previous piece instead: the same bytes to the same
+// place.
 #ifndef NERF_DMA_LEAN
 #define NERF_DMA_LEAN 1
 #endif
@@ -857,15 +1043,15 @@ __device__ __forceinline__ void fetch_piece_lean(const DmaLean& d) {
   constexpr int NU = (NCH + P::WAVES - 1) / P::WAVES;
   constexpr uint32_t GOFF = (uint32_t)(C0 + P::WAVES * I) * 1024u, LOFF = (uint32_t)(SLOT_OFF + P::WAVES * I * 1024);
   static_assert(NCH % P::WAVES == 0 || NU >= 2, "a one-piece group with surplus waves");
-  uint32_t tmp;
   if constexpr (I + 1 < NU || NCH % P::WAVES == 0) {
-    asm volatile("s_add_u32 m0, %1, %3\n\tv_add_u32 %0, %4, %2\n\tglobal_load_lds_dwordx4 %0, %5"
-                 : "=&v"(tmp) : "s"(d.swave), "v"(d.vlane), "i"(LOFF), "i"(GOFF), "s"(d.gbase) : "memory", "scc");
+    const uint32_t voff = d.vlane + GOFF;
+    asm volatile("s_add_u32 m0, %1, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %3"
+                 :: "v"(voff), "s"(d.swave), "i"(LOFF), "s"(d.gbase) : "memory", "scc");
   } else {
     const uint32_t adj = d.wave_u + P::WAVES * I > (uint32_t)(NCH - 1) ? (uint32_t)P::WAVES * 1024u : 0u;
-    asm volatile("s_add_u32 m0, %1, %3\n\tv_add_u32 %0, %4, %2\n\tglobal_load_lds_dwordx4 %0, %5"
-                 : "=&v"(tmp) : "s"(d.swave - adj), "v"(d.vlane), "i"(LOFF), "s"(GOFF - adj), "s"(d.gbase)
-                 : "memory", "scc");
+    const uint32_t voff = d.vlane + (GOFF - adj);
+    asm volatile("s_add_u32 m0, %1, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %3"
+                 :: "v"(voff), "s"(d.swave - adj), "i"(LOFF), "s"(d.gbase) : "memory", "scc");
   }
 }
 template <class P, int C0, int NCH, int SLOT_OFF>
@@ -1057,6 +1243,9 @@ struct FwdWave {
   using Tile = typename P::Tile;
   static constexpr int CH = P::CH;
   static_assert(!HALF || (P::KIND == K_BF16X3 && STORE), "half stores: bf16x3 training forward only");
+  static_assert(finish_schedule_violation<P, 0, DENSITY>() == 0,
+                "finish placement (NERF_FINISH_PARTS_* / NERF_FINISH_DELAY) reads a tile pair before its finish part "
+                "writes it, or reads a reassigned pend (FinishSchedule)");
   static constexpr int SCH = HALF ? 2 : P::CH;  // chunks stored per tile
   using GT = GroupTable<0, DENSITY, P::CH>;
 
@@ -1069,6 +1258,7 @@ struct FwdWave {
   float px, py, pz, dx, dy, dz;
   Tile X[2], D, Ha[8], Hb[8];
   uint32_t mw[4];
+  uint32_t one16;   // 0x00010001 in an SGPR, opaque to hipcc (nonzero_bf16x2)
   float alpha, rgb0, rgb1, rgb2;
   lds_cu4* wb;      // current group's slot + 16 h (bias reads)
   uint4 bias[4];
@@ -1084,6 +1274,7 @@ struct FwdWave {
     h = lane >> 5;
     wblock = blk * P::WAVES + wave;
     m = wblock * 32 + (lane & 31);
+    one16 = opaque_one16();
     dl = DmaLean{a.wpack, (uint32_t)(lane * 16 + wave * 1024),
                  (uint32_t)__builtin_amdgcn_readfirstlane(lds_base + (uint32_t)wave * 1024u),
                  (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)wave)};
@@ -1101,18 +1292,19 @@ struct FwdWave {
                                                             wave, lane);
   }
 
-  // input tile t of layer L (mlp_tables.h: Ha/Hb ping-pong, PE tiles X / D)
-  template <int L, int t> __device__ __forceinline__ const Tile& in_tile_L() const {
-    if constexpr (L == L0) return X[t];
-    else if constexpr (L == L5) { if constexpr (t < 2) return X[t]; else return Ha[t - 2]; }
-    else if constexpr (L == LV) { if constexpr (t < 8) return Ha[t]; else return D; }
-    else if constexpr (L == LRGB) return Hb[t];
-    else if constexpr (L == L1 || L == L3 || L == L7) return Ha[t];
-    else return Hb[t];  // L2, L4, L6, LFA
+  // register tile slot S (TileSlot: Ha/Hb ping-pong, PE tiles X / D); layer L reads
+  // slot<fwd_in_slot(L, t)>, its finish writes slot<fwd_out_slot(L, n)>
+  template <int S> __device__ __forceinline__ Tile& slot() {
+    if constexpr (S >= TS_HA && S < TS_HB) return Ha[S - TS_HA];
+    else if constexpr (S >= TS_HB && S < TS_X) return Hb[S - TS_HB];
+    else if constexpr (S == TS_X || S == TS_X + 1) return X[S - TS_X];
+    else {
+      static_assert(S == TS_D, "forward tile slot");
+      return D;
+    }
   }
-  template <int L> __device__ __forceinline__ Tile* out_arr() {
-    if constexpr (L == L0 || L == L2 || L == L4 || L == L6 || L == LFA) return Ha;
-    else return Hb;  // L1, L3, L5, L7, LV
+  template <int L, int t> __device__ __forceinline__ const Tile& in_tile_L() {
+    return slot<fwd_in_slot(L, t)>();
   }
 
   // vector-memory stores issued by unit u's finish
@@ -1137,7 +1329,7 @@ struct FwdWave {
     constexpr int K0 = 8 * p / NP, K1 = 8 * (p + 1) / NP;
     constexpr bool LASTP = p == NP - 1;
     if constexpr (L <= L7 || L == LV) {
-      Tile& out = out_arr<L>()[n];
+      Tile& out = slot<fwd_out_slot(L, n)>();
       uint32_t bits = 0;  // this tile's mask bits (mask_bit layout)
       sfor<K1 - K0>([&](auto kk) {
         constexpr int k = K0 + decltype(kk)::value;
@@ -1147,7 +1339,7 @@ struct FwdWave {
           // bits k / 16 + k from the packed result (as the bf16x3 path, NERF_PACKED_MASK)
           const uint32_t d = relu_bf16x2(pack_bf16(a0, a1));
           if constexpr (STORE && NERF_PACKED_MASK) {
-            bits |= nonzero_bf16x2(d) << k;
+            bits |= nonzero_bf16x2(d, one16) << k;
           } else if constexpr (STORE) {
             bits |= (a0 > 0.f ? 1u : 0u) << mask_bit(2 * k);
             bits |= (a1 > 0.f ? 1u : 0u) << mask_bit(2 * k + 1);
@@ -1159,7 +1351,7 @@ struct FwdWave {
           if constexpr (STORE && P::KIND == K_BF16X3 && NERF_PACKED_MASK) {
             // bit k / 16 + k = the pair's hi halves non-zero: the same bits as y > 0, since RNE keeps
             // every positive fp32 above 2^-134 non-zero in bf16 (pre-activations that small do not occur)
-            bits |= nonzero_bf16x2(pack_bf16(__int_as_float(y0), __int_as_float(y1))) << k;
+            bits |= nonzero_bf16x2(pack_bf16(__int_as_float(y0), __int_as_float(y1)), one16) << k;
           } else if constexpr (STORE) {
             bits |= min((uint32_t)y0, 1u) << mask_bit(2 * k);
             bits |= min((uint32_t)y1, 1u) << mask_bit(2 * k + 1);
@@ -1179,7 +1371,7 @@ struct FwdWave {
       }
     } else if constexpr (L == LFA) {
       if constexpr (n < 8) {  // feature_linear: no activation
-        Tile& out = Ha[n];
+        Tile& out = slot<fwd_out_slot(L, n)>();
         sfor<K1 - K0>([&](auto kk) {
           constexpr int k = K0 + decltype(kk)::value;
           P::set_pair(out, k, acc[2 * k], acc[2 * k + 1]);
@@ -1201,7 +1393,7 @@ struct FwdWave {
     while (!(GT::t.g[g].u0 <= u && u < GT::t.g[g].u0 + GT::t.g[g].n)) ++g;
     return g;
   }
-  template <int u, int t> __device__ __forceinline__ const Tile& in_tile() const {
+  template <int u, int t> __device__ __forceinline__ const Tile& in_tile() {
     return in_tile_L<fwd_unit_layer(u), t>();
   }
   // the unit's bias chunk (rows 8q + 4h + {0..3} = lane 2q + h) is the MFMA chain's
@@ -1356,6 +1548,9 @@ struct DxWave {
   using Tile = typename P::Tile;
   static constexpr int CH = P::CH;
   using GT = GroupTable<1, false, P::CH>;
+  static_assert(finish_schedule_violation<P, 1, false>() == 0,
+                "finish placement (NERF_FINISH_PARTS_* / NERF_FINISH_DELAY) reads a tile pair before its finish part "
+                "writes it, or reads a reassigned pend (FinishSchedule)");
 
   const DxArgs& a;
   const uint4* gw;
@@ -1394,17 +1589,18 @@ struct DxWave {
   }
   static __host__ __device__ constexpr int unit_stores(int) { return CH; }
 
-  template <int s, int t> __device__ __forceinline__ const Tile& in_tile_S() const {
-    if constexpr (s == B_RGB) return G;
-    else if constexpr (s == B_V) return Hb[t];
-    else if constexpr (s == B_FA) { if constexpr (t < 8) return Ha[t]; else return DA; }
-    else if constexpr (s == B_7 || s == B_5 || s == B_3 || s == B_1) return Hb[t];
-    else return Ha[t];  // B_6, B_4, B_2
+  // register tile slot S (TileSlot: Ha/Hb ping-pong, seeds G / DA); stage s reads
+  // slot<bwd_in_slot(s, t)>, its finish writes slot<bwd_out_slot(s, j)>
+  template <int S> __device__ __forceinline__ Tile& slot() {
+    if constexpr (S >= TS_HA && S < TS_HB) return Ha[S - TS_HA];
+    else if constexpr (S >= TS_HB && S < TS_X) return Hb[S - TS_HB];
+    else if constexpr (S == TS_G) return G;
+    else {
+      static_assert(S == TS_DA, "dX tile slot");
+      return DA;
+    }
   }
-  template <int s> __device__ __forceinline__ Tile* out_arr() {
-    if constexpr (s == B_RGB || s == B_FA || s == B_6 || s == B_4 || s == B_2) return Hb;
-    else return Ha;  // B_V, B_7, B_5, B_3, B_1
-  }
+  template <int s, int t> __device__ __forceinline__ const Tile& in_tile_S() { return slot<bwd_in_slot(s, t)>(); }
   // (dz tile, mask group or -1) of output tile j of stage s
   static __host__ __device__ constexpr int dz_tile(int s, int j) {
     return s == B_RGB ? ZT_V + j : s == B_V ? ZT_F + j : s == B_FA ? ZT_H + 56 + j : ZT_H + 8 * (bwd_fwd_layer(s) - 1) + j;
@@ -1420,7 +1616,7 @@ struct DxWave {
   }
 
   // ---- group_body hooks
-  template <int u, int t> __device__ __forceinline__ const Tile& in_tile() const {
+  template <int u, int t> __device__ __forceinline__ const Tile& in_tile() {
     return in_tile_S<bwd_unit_stage(u), t>();
   }
   template <int u> __device__ __forceinline__ void prefetch() {}
@@ -1448,7 +1644,7 @@ struct DxWave {
       const u16x2 t = __builtin_bit_cast(u16x2, w) << (u16x2){SH, SH};
       return __builtin_bit_cast(uint32_t, __builtin_bit_cast(i16x2, t) >> (i16x2){15, 15});
     };
-    Tile& out = out_arr<s>()[j];
+    Tile& out = slot<bwd_out_slot(s, j)>();
     sfor<K1 - K0>([&](auto kk) {
       constexpr int k = K0 + decltype(kk)::value;
       if constexpr (P::KIND == K_BF16) {

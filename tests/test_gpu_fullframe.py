@@ -18,7 +18,8 @@ march -- and is compared with NO exclusions:
     sample moved across a CDF bin by the coarse net's ~1e-5 relative error, which an exact
     (fp64) MLP does not move by more than 1.4e-4 (tools/fullframe_conditioning.py,
     profiles/r5/fullframe_conditioning.json); bf16 (operands rounded to bf16): >= 95 % within 2e-3,
-    its documented non-conforming tier (DESIGN.md section 5);
+    its documented non-conforming tier, held to 1.5x its own measurement
+    (max error, fraction beyond 2e-3 and row-sum error per key; uint8 frame; query count);
   * every row sum within 800 x the per-value bound (so every row of the frame is covered, not
     only the sampled rays);
   * the uint8 frame (clip(rgb) x 255, truncated): fp32 / bf16x3 / bf16x3f every pixel within
@@ -48,9 +49,22 @@ CONTRACT = 2e-3  # north_star: rgb/depth within 2e-3 for an MLP below fp32
 # fraction identical)
 BOUNDS = {"fp32": (1e-4, 1.0, 1e-4, 1, 0.999),
           "bf16x3": (1e-4, 0.95, CONTRACT, 1, 0.999),
-          "bf16x3f": (1e-4, 0.95, CONTRACT, 1, 0.999),
-          "bf16": (CONTRACT, 0.95, 1.0, 255, 0.94)}  # (measured: 97.8-99.5 % within 2e-3, frame 95.4 % identical)
-TIERS = list(BOUNDS)
+          "bf16x3f": (1e-4, 0.95, CONTRACT, 1, 0.999)}
+# bf16 (operands rounded to bf16: the documented non-conforming tier) is held to its own measurement
+# instead (round 6, gpurun_out/r6/fullframe.log; bf16 is bit-reproducible run to run and box to box, so
+# a bound 1.5x the measurement trips on a regression, not on noise): per key (max error, fraction of the
+# sampled values beyond 2e-3, largest row-sum error), per frame (largest uint8 difference, pixels more than
+# one level off), and the march's query-count offset from the reference's.
+BF16_MEASURED = {
+    "render": {"keys": {"rgb_map_c": (1.8e-2, 0.0157, 0.42), "depth_map_c": (1.0e-1, 0.0217, 1.3),
+                        "acc_map_c": (2.1e-2, 0.0085, 0.34), "rgb_map_f": (1.8e-1, 0.0151, 0.73),
+                        "depth_map_f": (7.5e-1, 0.0225, 2.0), "acc_map_f": (1.5e-1, 0.0039, 0.52)},
+               "u8_max": 121, "u8_px_over_1": 4183},
+    "march": {"keys": {"rgb_map_f": (1.1e-2, 0.0076, 0.38), "depth_map_f": (3.9e-2, 0.0125, 0.52),
+                       "acc_map_f": (1.0e-2, 0.0049, 0.14)},
+              "u8_max": 5, "u8_px_over_1": 564, "queried_offset": 3979}}
+BF16_MARGIN = 1.5
+TIERS = list(BOUNDS) + ["bf16"]
 
 
 @pytest.fixture(scope="module")
@@ -86,29 +100,37 @@ def renderer(cuda):
 
 def _compare(out, g4, prefix, keys, dtype):
     pix = torch.from_numpy(g4["pix"]).to(out[keys[0]].device)
-    tol, frac_min, maxerr, max_levels, ident_min = BOUNDS[dtype]
     report = {}
     for k in keys:
         full = out[k]
         assert full.shape[0] == H * W, (k, tuple(full.shape))
         got, ref = full[pix].cpu().numpy(), g4[f"{prefix}_{k}"]
         err = np.abs(got.astype(np.float64) - ref)
-        frac = float((err <= tol).mean())
-        report[k] = (float(err.max()), frac, float((err <= CONTRACT).mean()))
-        assert err.max() <= maxerr and frac >= frac_min, (prefix, k, dtype, err.max(), frac)
         rows = full.double().reshape(H, W, -1).sum(1).cpu().numpy()
-        rref = g4[f"{prefix}_rowsum_{k}"].reshape(H, -1)
-        rerr = float(np.abs(rows - rref).max())
-        report[k] += (rerr,)
-        if dtype != "bf16":
-            assert rerr <= W * maxerr, (prefix, k, dtype, rerr)
+        rerr = float(np.abs(rows - g4[f"{prefix}_rowsum_{k}"].reshape(H, -1)).max())
+        over = float((err > CONTRACT).mean())
+        report[k] = (float(err.max()), float((err <= 1e-4).mean()), 1 - over, rerr)
+        if dtype == "bf16":
+            mx, ov, rw = BF16_MEASURED[prefix]["keys"][k]
+            assert err.max() <= BF16_MARGIN * mx and over <= BF16_MARGIN * ov and rerr <= BF16_MARGIN * rw, \
+                (prefix, k, dtype, err.max(), over, rerr)
+            continue
+        tol, frac_min, maxerr, _, _ = BOUNDS[dtype]
+        assert err.max() <= maxerr and float((err <= tol).mean()) >= frac_min, (prefix, k, dtype, err.max())
+        assert rerr <= W * maxerr, (prefix, k, dtype, rerr)
     print(f"\n{prefix} {dtype}: " + ", ".join(f"{k} max {m:.1e} (<= 1e-4: {f:.4f}, <= 2e-3: {c:.4f}, row {r:.1e})"
                                            for k, (m, f, c, r) in report.items()))
     img = (out["rgb_map_f"].clamp(0, 1) * 255).to(torch.uint8).reshape(H, W, 3).cpu().numpy()
     d = np.abs(img.astype(int) - g4[f"{prefix}_frame_u8"].astype(int))
+    over1 = int((d.max(-1) > 1).sum())
     print(f"{prefix} {dtype} uint8 frame: max {d.max()}, identical {(d == 0).mean():.5f}, "
-          f"within one level {(d <= 1).mean():.6f}, pixels off by > 1: {int((d.max(-1) > 1).sum())}")
-    assert d.max() <= max_levels and (d == 0).mean() >= ident_min, (prefix, dtype, d.max(), (d == 0).mean())
+          f"within one level {(d <= 1).mean():.6f}, pixels off by > 1: {over1}")
+    if dtype == "bf16":
+        m = BF16_MEASURED[prefix]
+        assert d.max() <= BF16_MARGIN * m["u8_max"] and over1 <= BF16_MARGIN * m["u8_px_over_1"], (prefix, d.max(), over1)
+    else:
+        _, _, _, max_levels, ident_min = BOUNDS[dtype]
+        assert d.max() <= max_levels and (d == 0).mean() >= ident_min, (prefix, dtype, d.max(), (d == 0).mean())
 
 
 @pytest.mark.parametrize("dtype", TIERS)
@@ -139,4 +161,5 @@ def test_config4_full_frame_march(g4, frame, renderer, dtype):
     _compare(out, g4, "march", MARCH_KEYS, dtype)
     ref_q = int(g4["march_queried"])
     print(f"march {dtype}: queried {out['n_queried']} (reference {ref_q}), evaluated {out['n_evaluated']}")
-    assert abs(out["n_queried"] - ref_q) <= (16 if dtype != "bf16" else ref_q // 1000)  # (bf16 measured +3,979)
+    allow = 16 if dtype != "bf16" else int(BF16_MARGIN * BF16_MEASURED["march"]["queried_offset"])
+    assert abs(out["n_queried"] - ref_q) <= allow, (dtype, out["n_queried"] - ref_q)

@@ -720,16 +720,19 @@ def test_image_metrics_match_host_evaluator(cuda, ops, H, W, noise):
     assert abs(ssim - ref_ssim) < 1e-9, (ssim, ref_ssim)
 
 
+@pytest.mark.parametrize("M", [131101, 786432])
 @pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3", "bf16x3f"])
-def test_training_kernels_bitwise_deterministic(cuda, ops, seeded_state, dtype):
+def test_training_kernels_bitwise_deterministic(cuda, ops, seeded_state, dtype, M):
     """The training forward, dX and deterministic dW run twice on the same inputs write the same bytes: raw,
-    activation / mask / dz stores and the gradient.  The weight ring's hand-offs are counted waits and
-    barriers the compiler cannot see (csrc/mlp.hip); a late LDS read or an early DMA would show here as
-    run-to-run differences (r5: non-default finish-part placements did, NERF_FINISH_PARTS_BF16=2 / 8)."""
+    activation / mask / dz stores and the gradient, at a ragged size and at the fine net's config-3 launch.
+    The weight ring's hand-offs are counted waits and barriers the compiler cannot see (csrc/mlp.hip); a late
+    LDS read or an early DMA would show here as run-to-run differences.  (Round 5's finish-part sweep did see
+    them -- NERF_FINISH_PARTS_BF16 = 2 / 8 -- from an inline-asm VGPR write racing an MFMA's write-back and a
+    clamped finish part landing after the MFMA that reads its pair; both are now refused at build time:
+    tools/asm_check.py, FinishSchedule, tests/test_finish_schedule.py.)"""
     from nerf_amd._lib import check, lib, ptr, stream_of
     L = lib()
     g = torch.Generator().manual_seed(31)
-    M = 131101
     code = ops.dtype_code(dtype)
     packer = ops.PackedMLP([seeded_state[f"model.{n}"].to(cuda).contiguous() for n in ops.NET_PARAM_NAMES])
     pts = (torch.rand(M, 3, generator=g) * 3 - 1.5).to(cuda)
@@ -752,6 +755,28 @@ def test_training_kernels_bitwise_deterministic(cuda, ops, seeded_state, dtype):
     torch.cuda.synchronize()
     for k in ("raw", "act", "masks", "dz", "grad"):
         assert torch.equal(outs[0][k], outs[1][k]), (dtype, k)
+    if dtype != "fp32":  # (fp32 stores fp32 tiles: the bf16-pair check below does not apply)
+        _assert_masks_implied_by_act(outs[0]["act"], outs[0]["masks"], M)
+
+
+def _assert_masks_implied_by_act(act, masks, M):
+    """Every stored ReLU mask bit equals "the stored post-ReLU activation (its bf16 hi half) is non-zero":
+    mask dword n >> 1 of layer group l, bit 8 (n & 1) + (rho >> 1) + 16 (rho & 1) for register rho of tile n
+    (csrc/mlp.hip mask_bit, mlp_tables.h ActTile).  The round-5 mask race broke exactly this relation."""
+    nblk = (M + 255) // 256 * 8
+    nch = act.numel() // (nblk * 79 * 1024)  # chunks per stored tile-block: 2 (bf16 / bf16 halves) or 4 (hi, lo)
+    a = act.view(torch.int16).view(nblk, 79, nch, 64, 8)[:, :, :2]  # the bf16 (hi) chunks
+    got = masks.view(torch.int32).view(nblk, 9, 64, 4).to(torch.int64) & 0xFFFFFFFF
+    exp = torch.zeros_like(got)
+    rho = torch.arange(16, device=act.device)
+    bitpos = (rho >> 1) + 16 * (rho & 1)
+    for grp in range(9):
+        for n in range(8 if grp < 8 else 4):
+            tau = 3 + 8 * grp + n if grp < 8 else 75 + n
+            nz = (a[:, tau] != 0).permute(0, 2, 1, 3).reshape(nblk, 64, 16).to(torch.int64)
+            exp[:, grp, :, n >> 1] |= (nz << (bitpos + 8 * (n & 1))).sum(-1)
+    bad = (exp != got).sum(dim=(0, 2, 3))
+    assert int(bad.sum()) == 0, f"mask dwords not implied by the stored activations, per layer group: {bad.tolist()}"
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3", "bf16x3f", "bf16x6"])

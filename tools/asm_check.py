@@ -4,7 +4,14 @@
   * every counted `s_waitcnt vmcnt(N)` + s_barrier hand-off waits for the weight DMA:
     N <= vector-memory ops issued after the last global_load_lds before it,
   * no scratch (spills),
-  * no compiler code touches M0 (the lean LDS-DMA sets it without saving it).
+  * no compiler code touches M0 (the lean LDS-DMA sets it without saving it),
+  * no inline asm writes a VGPR (round 6): hipcc's hazard recognizer does not model the MFMA hazards of
+    an inline-asm VGPR write -- an asm output allocated to a dead lane of an accumulator whose MFMA is
+    still in flight is overwritten by the MFMA's late write-back (the round-5 mask race), so every VGPR
+    write must be compiler-placed (tools/mfma_war_scan.py measures the distances).
+The finish-part placement (which MFMA reads which register tile pair after which finish part wrote it)
+is a register dependence, invisible in the ISA as a hazard: it is checked at compile time by
+FinishSchedule (csrc/mlp.hip), a static_assert on every forward / dX instantiation.
     python tools/asm_check.py            (exit status 1 on a violation)
 """
 import os
@@ -14,11 +21,12 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ["fwd_kernel<nerf::mlp::PBF16, true, false, false>", "fwd_kernel<nerf::mlp::PBF16, false, false, false>",
-           "fwd_kernel<nerf::mlp::PBF16, false, true, false>", "fwd_kernel<nerf::mlp::PF32, true, false, false>",
-           "fwd_kernel<nerf::mlp::PF32, false, false, false>", "dx_kernel<nerf::mlp::PBF16>", "dx_kernel<nerf::mlp::PF32>",
-           "dw_kernel<nerf::mlp::PBF16>", "dw_kernel<nerf::mlp::PF32>",
-           "fwd_kernel<nerf::mlp::PF32, false, false, true>", "fwd_kernel<nerf::mlp::PBF16, false, false, true>"]
+# every MLP kernel instantiation the library builds: per precision the training, inference, density-only
+# and persistent forwards, dX and dW; the bf16x3f training forward (bf16 stores) and the bf16x6 forward
+KERNELS = [f"fwd_kernel<nerf::mlp::{p}, {a}>" for p in ("PF32", "PBF16", "PBF3")
+           for a in ("true, false, false", "false, false, false", "false, true, false", "false, false, true")] + \
+          ["fwd_kernel<nerf::mlp::PBF3, true, false, false, true>", "fwd_kernel<nerf::mlp::PBF6, false, false, false>"] + \
+          [f"{k}_kernel<nerf::mlp::{p}>" for k in ("dx", "dw") for p in ("PF32", "PBF16", "PBF3")]
 
 
 def build_asm(tmp, kernels=None):
@@ -63,7 +71,7 @@ def check(asm):
         since, waits, unsafe = None, 0, 0
         # the lean LDS-DMA (NERF_DMA_LEAN) writes M0 without saving it: no compiler code of the
         # kernel may read or write M0 (every M0 access must sit inside an inline-asm statement)
-        in_asm, m0_outside = False, 0
+        in_asm, m0_outside, asm_vgpr = False, 0, 0
         for l in lines:
             if ";;#ASMSTART" in l:
                 in_asm = True
@@ -71,6 +79,8 @@ def check(asm):
                 in_asm = False
             elif not in_asm and re.search(r"\bm0\b", l) and not l.strip().startswith(";"):
                 m0_outside += 1
+            elif in_asm and re.match(r"\s*v_\w+\s+v[\[\d]", l):
+                asm_vgpr += 1  # an instruction inside inline asm whose destination is a VGPR
         for i, l in enumerate(lines):
             t = l.strip()
             if t.startswith("global_load_lds"):
@@ -85,10 +95,10 @@ def check(asm):
         # loop (+ its guard) is its only backward branch
         persist = re.search(r"fwd_kernel\w*?ELb0ELb0ELb1E", name) is not None
         straight = "dw_kernel" in name or "dw_reduce" in name or not loops or (persist and len(loops) <= 2)
-        ok = straight and not unsafe and not m0_outside
+        ok = straight and not unsafe and not m0_outside and not asm_vgpr
         bad += not ok
         print(f"{'ok ' if ok else 'BAD'} {name[:70]:70s} loops={len(loops)} counted_waits={waits} unsafe={unsafe} "
-              f"m0_outside_asm={m0_outside}")
+              f"m0_outside_asm={m0_outside} asm_vgpr_writes={asm_vgpr}")
     for m in re.finditer(r"\.name:\s+(\S+)\n(?:.*\n){0,40}?\s+\.private_segment_fixed_size:\s+(\d+)", asm):
         if int(m.group(2)):
             bad += 1
