@@ -21,6 +21,7 @@
 #include "mlp_tables.h"
 
 #include <mutex>
+#include <type_traits>
 #include <utility>
 
 namespace nerf {
@@ -28,6 +29,7 @@ namespace mlp {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 
@@ -45,10 +47,12 @@ __device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
 // ------------------------------------------------------------------------------------
 // precision policies
 // ------------------------------------------------------------------------------------
-enum PKind { K_F32 = 0, K_BF16 = 1, K_BF16X3 = 2, K_BF16X6 = 3 };
+enum PKind { K_F32 = 0, K_BF16 = 1, K_BF16X3 = 2, K_BF16X6 = 3, K_BF16X3W = 4 };
 
 struct PF32 {
   static constexpr int KIND = K_F32;
+  using Acc = f32x16;     // one 32x32 accumulator tile
+  static constexpr int SPW = 32;  // samples per wave
   static constexpr int CH = 4;     // 1 KiB chunks per 32-feature input tile
   static constexpr int E = 4;      // elements per lane per chunk
   static constexpr int WAVES = 4;  // one wave per SIMD (<= 512 VGPR+AGPR)
@@ -98,6 +102,8 @@ struct PF32 {
 
 struct PBF16 {
   static constexpr int KIND = K_BF16;
+  using Acc = f32x16;     // one 32x32 accumulator tile
+  static constexpr int SPW = 32;  // samples per wave
   static constexpr int CH = 2;
   static constexpr int E = 8;
   static constexpr int WAVES = 8;  // two waves per SIMD (<= 256 VGPR)
@@ -155,6 +161,8 @@ struct PBF16 {
 // VGPRs, as fp32), stored as 4 KiB tile-blocks (hi 2 KiB then lo 2 KiB).
 struct PBF3 {
   static constexpr int KIND = K_BF16X3;
+  using Acc = f32x16;     // one 32x32 accumulator tile
+  static constexpr int SPW = 32;  // samples per wave
   static constexpr int CH = 4;
   static constexpr int E = 8;
   static constexpr int WAVES = 4;  // one wave per SIMD (16-VGPR tiles)
@@ -230,6 +238,8 @@ struct PBF3 {
 // chunks.  Weights: chunk 3q + p = part p (hi / mid / lo) of K half q.
 struct PBF6 {
   static constexpr int KIND = K_BF16X6;
+  using Acc = f32x16;     // one 32x32 accumulator tile
+  static constexpr int SPW = 32;  // samples per wave
   static constexpr int CH = 6;
   static constexpr int E = 8;
   static constexpr int WAVES = 4;  // one wave per SIMD (16-VGPR fp32 tiles)
@@ -283,6 +293,40 @@ struct PBF6 {
   }
 };
 
+// bf16x3 on v_mfma_f32_16x16x32_bf16 (round 6, the "wide" bf16x3 forward: 16 samples per wave, 8
+// waves per workgroup = two per SIMD, so that one wave's epilogue runs beside the other's MFMAs).  The
+// same arithmetic as PBF3 -- every fp32 operand split x = hi + lo, products hi*hi + hi*lo + lo*hi with
+// fp32 accumulation -- on 16-row units (mlp_tables.h fwd16_*).  A chunk is 16 weight rows x one 32-feature
+// K-block: chunk 0 the hi halves, chunk 1 the lo halves; a Tile is one K-block of the B operand (8 hi +
+// 8 lo bf16 per lane, 8 VGPRs), the accumulator 4 fp32.  Forward only: the bf16x3 dX / dW and the bf16
+// backward of bf16x3f read its training stores, which it writes in the 32x32 fragment layout.
+struct PBF3W {
+  static constexpr int KIND = K_BF16X3W;
+  using Acc = f32x4;
+  static constexpr int SPW = 16;
+  static constexpr int CH = 2;
+  static constexpr int E = 8;
+  static constexpr int WAVES = 8;
+  static constexpr int ESIZE = 4;
+  static constexpr int SPL = 8;
+  static constexpr int PE = 2;  // PE_POLY, as PBF3
+  using Store = __bf16;
+  struct Tile { bf16x8 hi, lo; };
+  static __device__ __forceinline__ f32x4 mma(uint4 a, const Tile& b, int c, f32x4 acc) {
+    const bf16x8 av = __builtin_bit_cast(bf16x8, a);
+    if (c == 0) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b.hi, acc, 0, 0, 0);
+      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b.lo, acc, 0, 0, 0);
+    }
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b.hi, acc, 0, 0, 0);
+  }
+  static __host__ __device__ constexpr int rho_of(int, int e) { return e; }  // (a chunk reads the whole K-block)
+  static __device__ __forceinline__ Store cvt_c(float x, int c) {
+    const __bf16 h = (__bf16)x;
+    return c == 0 ? h : (__bf16)(x - (float)h);
+  }
+};
+
 // ReLU-mask bit of accumulator register rho of a tile: the tile's 16 bits sit at positions
 // (rho >> 1) + 16 (rho & 1) of a dword (bf16 pair k = registers 2k, 2k+1 -> bits k, 16 + k),
 // and two tiles n, n + 1 share one dword, the odd one shifted up by 8.
@@ -314,7 +358,7 @@ __device__ __forceinline__ uint32_t opaque_one16() {
   return one;
 }
 
-template <class P> __host__ __device__ constexpr int samples_per_block() { return P::WAVES * 32; }
+template <class P> __host__ __device__ constexpr int samples_per_block() { return P::WAVES * P::SPW; }
 constexpr int M_ALIGN = 256;  // activation stores are padded to this many samples
 
 // ------------------------------------------------------------------------------------
@@ -322,12 +366,18 @@ constexpr int M_ALIGN = 256;  // activation stores are padded to this many sampl
 //   forward unit u: fwd_unit_tiles(u) * CH weight chunks, then 1 bias chunk (32 fp32)
 //   backward unit u: bwd_unit_tiles(u) * CH weight chunks
 // ------------------------------------------------------------------------------------
+// DIR 0: forward units, 1: dX-chain units, 2: 16-row forward units (PBF3W)
+__host__ __device__ constexpr int num_units(int dir) { return dir == 0 ? NUNIT_FWD : dir == 1 ? NUNIT_BWD : NUNIT_FWD16; }
 __host__ __device__ constexpr int fwd_unit_chunks(int u, int ch) { return fwd_unit_tiles(u) * ch + 1; }
+__host__ __device__ constexpr int fwd16_unit_chunks(int u, int ch) { return fwd16_unit_tiles(u) * ch + 1; }
+__host__ __device__ constexpr int fwd16_unit_chunk_off(int u, int ch) { return fwd16_unit_tile_off(u) * ch + u; }
 __host__ __device__ constexpr int fwd_unit_chunk_off(int u, int ch) { return fwd_unit_tile_off(u) * ch + u; }
 __host__ __device__ constexpr int bwd_unit_chunks(int u, int ch) { return bwd_unit_tiles(u) * ch; }
 __host__ __device__ constexpr int bwd_unit_chunk_off(int u, int ch) { return bwd_unit_tile_off(u) * ch; }
 __host__ __device__ constexpr int64_t total_chunks(int ch, int dir) {
-  return dir == 0 ? (int64_t)FWD_TILES * ch + NUNIT_FWD : (int64_t)BWD_TILES * ch;
+  return dir == 0 ? (int64_t)FWD_TILES * ch + NUNIT_FWD
+       : dir == 1 ? (int64_t)BWD_TILES * ch
+       : (int64_t)FWD16_TILES * ch + NUNIT_FWD16;
 }
 
 struct ParamPtrs { const float* p[NPARAM]; };
@@ -335,12 +385,13 @@ struct ParamPtrs { const float* p[NPARAM]; };
 // first chunk of every unit (+ the end), evaluated at compile time and passed by value:
 // the unit of a chunk is then a scan of kernel arguments, not a runtime walk of the
 // constexpr layout functions (which are loops)
-struct UnitOffsets { int off[NUNIT_FWD + 1]; };
+struct UnitOffsets { int off[NUNIT_MAX + 1]; };
 template <int CH, int DIR>
 constexpr UnitOffsets unit_offsets() {
   UnitOffsets t{};
-  const int nu = DIR == 0 ? NUNIT_FWD : NUNIT_BWD;
-  for (int u = 0; u <= nu; ++u) t.off[u] = DIR == 0 ? fwd_unit_chunk_off(u, CH) : bwd_unit_chunk_off(u, CH);
+  const int nu = num_units(DIR);
+  for (int u = 0; u <= nu; ++u)
+    t.off[u] = DIR == 0 ? fwd_unit_chunk_off(u, CH) : DIR == 1 ? bwd_unit_chunk_off(u, CH) : fwd16_unit_chunk_off(u, CH);
   return t;
 }
 
@@ -353,10 +404,34 @@ __device__ __forceinline__ void pack_sources(int64_t i, const UnitOffsets& uo, W
   const int lane = (int)(i & 63);
   const int chunk = (int)(i >> 6);
   const int r = lane & 31, h = lane >> 5;
-  const int nunit = DIR == 0 ? NUNIT_FWD : NUNIT_BWD;
+  const int nunit = num_units(DIR);
   int u = 0;
   for (int k = 1; k < nunit; ++k) u += uo.off[k] <= chunk ? 1 : 0;
   const int within = chunk - uo.off[u];
+  if (DIR == 2) {
+    // 16-row unit (PBF3W): lane l = r16 + 16 g holds weight row r16 of the unit, the 8 features
+    // k16_feat(g, e) of K-block t; chunk c = 0 the hi, 1 the lo halves.  Bias chunk: lanes 0..3 hold
+    // rows 4 lane + e (the accumulator's rows of lane group g = lane), rest zero.
+    const int L = fwd16_unit_layer(u), m = u - fwd16_unit_first(L);
+    const int w = fwd16_out_weight(L, m);
+    if (within == fwd16_unit_tiles(u) * P::CH) {
+      for (int e = 0; e < 4; ++e) {
+        const int row = lane * 4 + e;
+        const bool ok = lane < 4 && row < fwd16_out_valid(L, m);
+        bias(e, ok ? w + 1 : -1, (int64_t)(fwd16_out_row0(L, m) + row));
+      }
+      return;
+    }
+    const int t = within / P::CH, c = within % P::CH, r16 = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int f = k16_feat(g, e);
+      const bool ok = r16 < fwd16_out_valid(L, m) && f < fwd_in_valid(L, t);
+      weight(e, ok ? w : -1,
+             ok ? (int64_t)(fwd16_out_row0(L, m) + r16) * weight_K(w) + fwd_in_colbase(L, t) + f : (int64_t)0, c);
+    }
+    return;
+  }
   if (DIR == 0 && within == fwd_unit_tiles(u) * P::CH) {
     // bias chunk: lanes 0..7 hold the 32 biases of the unit's output rows, rest zero
     const int L = fwd_unit_layer(u), n = u - fwd_unit_first(L);
@@ -543,28 +618,30 @@ constexpr int GROUP_MAX = 8;   // units per group
 struct Group { int u0, n, c0, nch; };  // first unit, units, first chunk, chunks
 
 // DIR 0: forward units (DENSITY: trunk + alpha only, occupancy_grid.py:60 reads raw[...,3]);
-// DIR 1: dX-chain units
+// DIR 1: dX-chain units; DIR 2: 16-row forward units (PBF3W)
 template <int DIR, bool DENSITY>
 __host__ __device__ constexpr bool unit_used(int u) {
-  return DIR != 0 || !DENSITY || u < fwd_unit_first(LFA) || u == fwd_unit_first(LFA) + 8;
+  return DIR == 1 || !DENSITY ||
+         (DIR == 0 ? (u < fwd_unit_first(LFA) || u == fwd_unit_first(LFA) + 8)
+                   : (u < fwd16_unit_first(LFA) || u == fwd16_unit_first(LFA) + 16));
 }
 template <int DIR> __host__ __device__ constexpr int unit_seg(int u) {
-  return DIR == 0 ? fwd_unit_layer(u) : bwd_unit_stage(u);
+  return DIR == 0 ? fwd_unit_layer(u) : DIR == 1 ? bwd_unit_stage(u) : fwd16_unit_layer(u);
 }
 template <int DIR> __host__ __device__ constexpr int unit_chunks(int u, int ch) {
-  return DIR == 0 ? fwd_unit_chunks(u, ch) : bwd_unit_chunks(u, ch);
+  return DIR == 0 ? fwd_unit_chunks(u, ch) : DIR == 1 ? bwd_unit_chunks(u, ch) : fwd16_unit_chunks(u, ch);
 }
 template <int DIR> __host__ __device__ constexpr int unit_chunk_off(int u, int ch) {
-  return DIR == 0 ? fwd_unit_chunk_off(u, ch) : bwd_unit_chunk_off(u, ch);
+  return DIR == 0 ? fwd_unit_chunk_off(u, ch) : DIR == 1 ? bwd_unit_chunk_off(u, ch) : fwd16_unit_chunk_off(u, ch);
 }
 
 // greedy grouping: consecutive used units of one segment while the slot has room
 template <int DIR, bool DENSITY, int CH>
 struct Groups {
-  Group g[NUNIT_FWD > NUNIT_BWD ? NUNIT_FWD : NUNIT_BWD];
+  Group g[NUNIT_MAX];
   int n;
   __host__ __device__ constexpr Groups() : g(), n(0) {
-    const int NU = DIR == 0 ? NUNIT_FWD : NUNIT_BWD;
+    const int NU = num_units(DIR);
     int u = 0;
     while (u < NU) {
       if (!unit_used<DIR, DENSITY>(u)) {
@@ -632,7 +709,7 @@ __host__ __device__ constexpr int handoff_vmcnt(int g, StoresFn stores, int prol
 
 struct Step { int j, u, t, c, off, kin, len; bool first, last; };
 template <int DIR> __host__ __device__ constexpr int unit_tiles(int u) {
-  return DIR == 0 ? fwd_unit_tiles(u) : bwd_unit_tiles(u);
+  return DIR == 0 ? fwd_unit_tiles(u) : DIR == 1 ? bwd_unit_tiles(u) : fwd16_unit_tiles(u);
 }
 template <int DIR, bool DENSITY, int CH>
 __host__ __device__ constexpr int group_steps(int g) {
@@ -714,8 +791,12 @@ __host__ __device__ constexpr bool finished_in_group(int g, int u) {
 #ifndef NERF_FINISH_PARTS_BF3
 #define NERF_FINISH_PARTS_BF3 8  // with NERF_DMA_SPREAD_BF3 3: bf16x3 forward 1.70 -> 1.58 ms, training
 #endif                           // forward 1.97 -> 1.88, dX 1.73 -> 1.65 at 524,288 samples (r4)
+#ifndef NERF_FINISH_PARTS_BF3W
+#define NERF_FINISH_PARTS_BF3W 2  // (a 16x16 tile's 2 register pairs)
+#endif
 template <class P> __host__ __device__ constexpr int finish_parts() {
-  return P::KIND == K_F32 ? NERF_FINISH_PARTS_F32 : P::KIND == K_BF16 ? NERF_FINISH_PARTS_BF16 : NERF_FINISH_PARTS_BF3;
+  return P::KIND == K_F32 ? NERF_FINISH_PARTS_F32 : P::KIND == K_BF16 ? NERF_FINISH_PARTS_BF16
+       : P::KIND == K_BF16X3W ? NERF_FINISH_PARTS_BF3W : NERF_FINISH_PARTS_BF3;
 }
 // DMA spread.  0: the next group's LDS-DMA pieces (up to 18 per wave, ~7 instructions each)
 // are issued as one burst at the group's start; S > 0: piece i at step i (NS / S) / NF of the
@@ -729,8 +810,12 @@ template <class P> __host__ __device__ constexpr int finish_parts() {
 #ifndef NERF_DMA_SPREAD_BF3
 #define NERF_DMA_SPREAD_BF3 3
 #endif
+#ifndef NERF_DMA_SPREAD_BF3W
+#define NERF_DMA_SPREAD_BF3W 3
+#endif
 template <class P> __host__ __device__ constexpr int dma_spread() {
-  return PF != 1 ? 0 : P::KIND == K_F32 ? NERF_DMA_SPREAD_F32 : P::KIND == K_BF16 ? NERF_DMA_SPREAD_BF16 : NERF_DMA_SPREAD_BF3;
+  return PF != 1 ? 0 : P::KIND == K_F32 ? NERF_DMA_SPREAD_F32 : P::KIND == K_BF16 ? NERF_DMA_SPREAD_BF16
+       : P::KIND == K_BF16X3W ? NERF_DMA_SPREAD_BF3W : NERF_DMA_SPREAD_BF3;
 }
 
 // step (in group g) at which part p of unit u's finish is issued, or -1 when u is not
@@ -764,7 +849,7 @@ template <class P, int DIR, bool DENSITY, class StoresFn>
 __host__ __device__ constexpr int handoff_vmcnt_spread(int g, StoresFn unit_stores) {
   if (g + 1 >= GroupTable<DIR, DENSITY, P::CH>::t.n) return 0;  // (the last group: no hand-off)
   const int last = dma_piece_step<P, DIR, DENSITY>(g, group_dma_units<P, DIR, DENSITY>(g + 1) - 1);
-  const int NU = DIR == 0 ? NUNIT_FWD : NUNIT_BWD;
+  const int NU = num_units(DIR);
   int n = 0;
   for (int u = 0; u < NU; ++u) {
     const int s = part_step<P, DIR, DENSITY>(g, u, finish_parts<P>() - 1);
@@ -825,11 +910,19 @@ __host__ __device__ constexpr int bwd_out_slot(int s, int j) {
   return (s == B_RGB || s == B_FA || s == B_6 || s == B_4 || s == B_2) ? TS_HB + j : TS_HA + j;
 }
 template <int DIR> __host__ __device__ constexpr int unit_in_slot(int u, int t) {
-  return DIR == 0 ? fwd_in_slot(fwd_unit_layer(u), t) : bwd_in_slot(bwd_unit_stage(u), t);
+  return DIR == 0 ? fwd_in_slot(fwd_unit_layer(u), t)
+       : DIR == 1 ? bwd_in_slot(bwd_unit_stage(u), t)
+       : fwd_in_slot(fwd16_unit_layer(u), t);
 }
+// 16-row unit (DIR 2): output tile m fills half m & 1 (elements 4 (m & 1) .. + 3) of K-block slot m >> 1
 template <int DIR> __host__ __device__ constexpr int unit_out_slot(int u) {
   return DIR == 0 ? fwd_out_slot(fwd_unit_layer(u), u - fwd_unit_first(fwd_unit_layer(u)))
-                  : bwd_out_slot(bwd_unit_stage(u), u - bwd_unit_first(bwd_unit_stage(u)));
+       : DIR == 1 ? bwd_out_slot(bwd_unit_stage(u), u - bwd_unit_first(bwd_unit_stage(u)))
+       : fwd_out_slot(fwd16_unit_layer(u), (u - fwd16_unit_first(fwd16_unit_layer(u))) >> 1);
+}
+// the register pairs of its slot a unit's finish writes (a 32x32 tile: all 8; a 16-row unit: 2 of a K-block's 4)
+template <int DIR> __host__ __device__ constexpr int unit_out_pairs(int u) {
+  return DIR != 2 ? 0xFF : (((u - fwd16_unit_first(fwd16_unit_layer(u))) & 1) ? 0xC : 0x3);
 }
 // register pairs (bit k = registers 2k, 2k + 1) of a tile that MFMA chunk c reads / finish part p writes
 template <class P> __host__ __device__ constexpr int chunk_pairs(int c) {
@@ -840,11 +933,17 @@ template <class P> __host__ __device__ constexpr int chunk_pairs(int c) {
   }
   return m;
 }
+// pairs of an output tile: 8 (32x32 accumulator, 16 registers), 2 (16x16, 4 registers)
+template <class P> __host__ __device__ constexpr int tile_pairs() { return P::KIND == K_BF16X3W ? 2 : 8; }
 template <class P> __host__ __device__ constexpr int part_pairs(int p) {
-  constexpr int NP = finish_parts<P>();
+  constexpr int NP = finish_parts<P>(), TP = tile_pairs<P>();
   int m = 0;
-  for (int k = 8 * p / NP; k < 8 * (p + 1) / NP; ++k) m |= 1 << k;
+  for (int k = TP * p / NP; k < TP * (p + 1) / NP; ++k) m |= 1 << k;
   return m;
+}
+// the pairs of its slot part p of unit u writes
+template <class P, int DIR> __host__ __device__ constexpr int part_write_pairs(int u, int p) {
+  return DIR != 2 ? part_pairs<P>(p) : part_pairs<P>(p) << (unit_out_pairs<DIR>(u) == 0xC ? 2 : 0);
 }
 // Positions in the straight-line schedule: 4 * (global step) + phase, the phases of one step in
 // group_body's order: 0 DMA pieces, 1 pend / init + MFMA, 2 the previous unit's finish parts, 3 the
@@ -855,10 +954,10 @@ template <class P> __host__ __device__ constexpr int part_pairs(int p) {
 // after it was reassigned, 4 a finish part is never issued.
 template <class P, int DIR, bool DENSITY>
 struct FinishSchedule {
-  static constexpr int NU = DIR == 0 ? NUNIT_FWD : NUNIT_BWD;
+  static constexpr int NU = num_units(DIR);
   static constexpr int NP = finish_parts<P>();
-  int pos[NUNIT_FWD > NUNIT_BWD ? NUNIT_FWD : NUNIT_BWD][8];   // position of part p of unit u (-1: none)
-  int pend_at[NUNIT_FWD > NUNIT_BWD ? NUNIT_FWD : NUNIT_BWD];  // position at which `pend` takes unit u (-1)
+  int pos[NUNIT_MAX][8];   // position of part p of unit u (-1: none)
+  int pend_at[NUNIT_MAX];  // position at which `pend` takes unit u (-1)
   int violation;
   __host__ __device__ constexpr FinishSchedule() : pos(), pend_at(), violation(0) {
     const auto& T = GroupTable<DIR, DENSITY, P::CH>::t;
@@ -886,14 +985,25 @@ struct FinishSchedule {
   }
   __host__ __device__ constexpr int check() const {
     const auto& T = GroupTable<DIR, DENSITY, P::CH>::t;
-    int out[NUNIT_FWD > NUNIT_BWD ? NUNIT_FWD : NUNIT_BWD] = {}, next[NUNIT_FWD > NUNIT_BWD ? NUNIT_FWD : NUNIT_BWD] = {};
+    int out[NUNIT_MAX] = {}, opairs[NUNIT_MAX] = {}, pw[NUNIT_MAX][8] = {}, next_w[NUNIT_MAX][8] = {};
     for (int u = 0; u < NU; ++u) {
       out[u] = unit_used<DIR, DENSITY>(u) ? unit_out_slot<DIR>(u) : (int)TS_NONE;
-      next[u] = -1;
+      opairs[u] = finish_slot(out[u]) ? unit_out_pairs<DIR>(u) : 0;
+      for (int p = 0; p < NP; ++p) pw[u][p] = part_write_pairs<P, DIR>(u, p);
     }
-    for (int u = NU - 1; u >= 0; --u)  // next unit writing the same slot
-      for (int v = u + 1; v < NU && next[u] < 0; ++v)
-        if (finish_slot(out[u]) && out[v] == out[u]) next[u] = v;
+    {  // next_w[u][q]: the next unit after u that writes pair q of u's slot (-1: none)
+      int seen[TS_X][8] = {};
+      for (int sl = 0; sl < TS_X; ++sl)
+        for (int q = 0; q < 8; ++q) seen[sl][q] = -1;
+      for (int u = NU - 1; u >= 0; --u)
+        for (int q = 0; q < 8; ++q) {
+          next_w[u][q] = -1;
+          if ((opairs[u] >> q) & 1) {
+            next_w[u][q] = seen[out[u]][q];
+            seen[out[u]][q] = u;
+          }
+        }
+    }
     for (int u = 0; u < NU; ++u) {
       if (!unit_used<DIR, DENSITY>(u)) continue;
       for (int p = 0; p < NP; ++p) {
@@ -905,15 +1015,18 @@ struct FinishSchedule {
           if (pend_at[v] >= 0 && pend_at[v] < pos[u][p]) return 3;
       }
     }
-    int writer[TS_X] = {};  // last unit (in unit order, before the reading unit) whose output is the slot
-    for (int s = 0; s < TS_X; ++s) writer[s] = -1;
+    // writer[slot][pair]: the last unit (in unit order, before the reading unit) that writes the pair
+    int writer[TS_X][8] = {};
+    for (int sl = 0; sl < TS_X; ++sl)
+      for (int q = 0; q < 8; ++q) writer[sl][q] = -1;
     int base = 0;
     for (int g = 0; g < T.n; ++g) {
       const Group G = T.g[g];
       for (int j = 0; j < G.n; ++j) {
         const int u = G.u0 + j;
         for (int v = (j == 0 ? 0 : u - 1); v < u; ++v)
-          if (finish_slot(out[v])) writer[out[v]] = v;
+          for (int q = 0; q < 8; ++q)
+            if ((opairs[v] >> q) & 1) writer[out[v]][q] = v;
         const int nt = unit_tiles<DIR>(u);
         for (int t = 0; t < nt; ++t) {
           const int slot = unit_in_slot<DIR>(u, t);
@@ -921,14 +1034,18 @@ struct FinishSchedule {
             base += P::CH;
             continue;
           }
-          const int prod = writer[slot];
-          if (prod < 0) return 1;
           for (int c = 0; c < P::CH; ++c, ++base) {
             const int rpos = 4 * base + 1, cp = chunk_pairs<P>(c);
-            for (int p = 0; p < NP; ++p) {
-              if (!(part_pairs<P>(p) & cp)) continue;
-              if (pos[prod][p] >= rpos) return 1;
-              if (next[prod] >= 0 && pos[next[prod]][p] >= 0 && pos[next[prod]][p] < rpos) return 2;
+            for (int q = 0; q < 8; ++q) {
+              if (!((cp >> q) & 1)) continue;
+              const int prod = writer[slot][q];
+              if (prod < 0) return 1;
+              const int nv = next_w[prod][q];
+              for (int p = 0; p < NP; ++p) {
+                if (((pw[prod][p] >> q) & 1) && pos[prod][p] >= rpos) return 1;
+                // the next unit writing the pair must not write it before this read
+                if (nv >= 0 && ((pw[nv][p] >> q) & 1) && pos[nv][p] >= 0 && pos[nv][p] < rpos) return 2;
+              }
             }
           }
         }
@@ -962,7 +1079,7 @@ __device__ __forceinline__ void group_body(W& w, lds_cu4* wl) {
     ring[k] = as_uint4(wl[S.off * 64]);
   });
   w.template prefetch<G.u0>();
-  f32x16 acc;
+  typename P::Acc acc;
   sfor<NS>([&](auto kk) {
     constexpr int k = decltype(kk)::value;
     constexpr Step S = group_step<DIR, DENSITY, P::CH>(g, k);
@@ -1214,7 +1331,9 @@ __device__ __forceinline__ uint4* mask_slot(void* masks, int64_t wblock, int grp
 #ifndef NERF_KEEP_PE_BF3
 #define NERF_KEEP_PE_BF3 1
 #endif
-template <class P> __host__ __device__ constexpr bool keep_pe() { return P::KIND == K_BF16X3 && NERF_KEEP_PE_BF3; }
+template <class P> __host__ __device__ constexpr bool keep_pe() {
+  return (P::KIND == K_BF16X3 || P::KIND == K_BF16X3W) && NERF_KEEP_PE_BF3;
+}
 
 // ------------------------------------------------------------------------------------
 // forward: one wave = 32 samples through all 11 layers; activations stay in registers
@@ -1502,6 +1621,326 @@ struct FwdWave {
   }
 };
 
+// ------------------------------------------------------------------------------------
+// The wide bf16x3 forward (round 6, PBF3W): one wave = 16 samples on v_mfma_f32_16x16x32_bf16, 8 waves
+// per workgroup, two per SIMD.  The bf16x3 forward of the 32x32 kernels above holds 32 samples' hi / lo
+// activation tiles per wave in ~370 registers -- one wave per SIMD, so nothing feeds the matrix pipe
+// while a wave runs its epilogue (ReLU, hi / lo split, masks, stores) or waits on LDS; with 16 samples
+// a wave needs ~200 registers and the two waves of a SIMD overlap each other's epilogues and waits.
+// Same weight ring (2 x 72 KiB LDS slots, LDS-DMA one group ahead, counted hand-offs) and group
+// pipeline (group_body, finish parts, spread DMA) over 16-row units (DIR 2).
+//
+// Training stores go to the 32x32 fragment layout the dX / dW kernels read (mlp_tables.h "Training
+// stores"): a 32-sample tile-block spans the two waves of a SIMD pair (wave & 1 = its half of the
+// samples) and two 16-row output tiles (old chunk c = tile m & 1).  Old lane L = sample (L & 31) + 32 h
+// holds features 16 c + 4 h + {0..3} then 16 c + 8 + 4 h + {0..3}: exactly the 4 rows of this kernel's
+// lane (s, g = h) and of lane (s, g = h + 2) -- so every lane writes its 8 bytes (4 bf16) with one
+// global_store_dwordx2 at 16 L + 8 (g >> 1), no exchange.  The ReLU-mask bits of old lane L come from the
+// lanes l and l + 32 of one wave: combined with one v_permlane32_swap per mask dword at the layer's end.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void store8(char* p, uint32_t lo, uint32_t hi) {
+  if constexpr (NERF_DIAG_NO_STORE) return;
+  typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+  __builtin_nontemporal_store((u32x2v){lo, hi}, (u32x2v*)p);
+}
+__device__ __forceinline__ uint32_t get_dword(const bf16x8& v, int k) {
+  const uint4 u = __builtin_bit_cast(uint4, v);
+  return k == 0 ? u.x : k == 1 ? u.y : k == 2 ? u.z : u.w;
+}
+__device__ __forceinline__ void set_dword8(bf16x8& v, int k, uint32_t d) {
+  uint4 u = __builtin_bit_cast(uint4, v);
+  if (k == 0) u.x = d;
+  else if (k == 1) u.y = d;
+  else if (k == 2) u.z = d;
+  else u.w = d;
+  v = __builtin_bit_cast(bf16x8, u);
+}
+// position encoding of K-block TILE in the PBF3W B-operand layout: element e of lane group g is feature
+// 32 TILE + k16_feat(g, e); the same fp32 values as pe_tile<PBF3> (PE_POLY), split hi / lo
+template <class T> __device__ __forceinline__ T sel4(int g, T a0, T a1, T a2, T a3) {
+  return (g & 2) ? ((g & 1) ? a3 : a2) : ((g & 1) ? a1 : a0);  // (branch-free selects on the lane group)
+}
+template <int TILE, int NFREQ, int NVALID>
+__device__ __forceinline__ void pe_kblock(PBF3W::Tile& t, int g, float x0, float x1, float x2) {
+  constexpr double INV2PI = 0.15915494309189533576888376337251;
+  float v[8];
+  sfor<8>([&](auto ee) {
+    constexpr int e = decltype(ee)::value;
+    constexpr PeFeat F0 = pe_feat(32 * TILE + k16_feat(0, e), NFREQ, NVALID);
+    constexpr PeFeat F1 = pe_feat(32 * TILE + k16_feat(1, e), NFREQ, NVALID);
+    constexpr PeFeat F2 = pe_feat(32 * TILE + k16_feat(2, e), NFREQ, NVALID);
+    constexpr PeFeat F3 = pe_feat(32 * TILE + k16_feat(3, e), NFREQ, NVALID);
+    // every candidate is chosen at compile time; only the lane group selects among them
+    const float c0 = F0.dim == 0 ? x0 : F0.dim == 1 ? x1 : x2, c1 = F1.dim == 0 ? x0 : F1.dim == 1 ? x1 : x2;
+    const float c2 = F2.dim == 0 ? x0 : F2.dim == 1 ? x1 : x2, c3 = F3.dim == 0 ? x0 : F3.dim == 1 ? x1 : x2;
+    const float x = sel4(g, c0, c1, c2, c3);
+    float trig = 0.f;
+    if constexpr (F0.kind == 2 || F1.kind == 2 || F2.kind == 2 || F3.kind == 2) {
+      const double srev = sel4(g, INV2PI * (double)(1 << F0.k), INV2PI * (double)(1 << F1.k),
+                               INV2PI * (double)(1 << F2.k), INV2PI * (double)(1 << F3.k));
+      const double ph = sel4(g, F0.cos ? 0.25 : 0.0, F1.cos ? 0.25 : 0.0, F2.cos ? 0.25 : 0.0, F3.cos ? 0.25 : 0.0);
+      trig = pe_trig<PE_POLY>(x, srev, 0.f, ph, false);
+    }
+    v[e] = sel4(g, F0.kind == 2 ? trig : F0.kind == 1 ? x : 0.f, F1.kind == 2 ? trig : F1.kind == 1 ? x : 0.f,
+                F2.kind == 2 ? trig : F2.kind == 1 ? x : 0.f, F3.kind == 2 ? trig : F3.kind == 1 ? x : 0.f);
+  });
+  uint32_t hw[4], lw[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    hw[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
+    lw[k] = pack_bf16(v[2 * k] - __uint_as_float(hw[k] << 16), v[2 * k + 1] - __uint_as_float(hw[k] & 0xffff0000u));
+  }
+  t.hi = __builtin_bit_cast(bf16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
+  t.lo = __builtin_bit_cast(bf16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+}
+
+template <bool STORE, bool DENSITY, bool PERSIST = false, bool HALF = false>
+struct FwdWave16 {
+  using P = PBF3W;
+  using Tile = P::Tile;
+  using Acc = f32x4;
+  static constexpr int CH = P::CH;
+  static constexpr int SCH = HALF ? 2 : 4;  // chunks of a stored tile-block: bf16 hi (bf16x3f) or hi + lo
+  static constexpr int SST = HALF ? 1 : 2;  // 8-byte stores per output tile
+  using GT = GroupTable<2, DENSITY, P::CH>;
+  static_assert(finish_schedule_violation<P, 2, DENSITY>() == 0,
+                "finish placement (NERF_FINISH_PARTS_* / NERF_FINISH_DELAY) reads a tile pair before its finish part "
+                "writes it, or reads a reassigned pend (FinishSchedule)");
+
+  const FwdArgs& a;
+  uint32_t lds_base;
+  int lane, wave, s, g;
+  int64_t m;        // this lane's sample
+  int64_t wb32;     // the 32-sample block of the training stores
+  uint32_t st_off;  // byte offset of this lane's 8 bytes in a 1-KiB chunk of the stores
+  uint32_t lold;    // old-layout lane of the mask store: sample (16 (wave & 1) + s) + 32 (g & 1)
+  uint32_t gsh;     // 2 (g >> 1): offset of this lane's mask bits among an old register pair group
+  float px, py, pz, dx, dy, dz;
+  Tile X[2], D, Ha[8], Hb[8];
+  uint32_t mw[4];
+  uint32_t one16;
+  float alpha, rgb0, rgb1, rgb2;
+  lds_cu4* wbg;     // current group's slot + 16 g (bias reads)
+  uint4 bias;
+  Acc pend;
+  DmaLean dl;
+
+  __device__ __forceinline__ FwdWave16(const FwdArgs& args, const uint4* smem, int64_t blk, int tid) : a(args) {
+    lds_base = (uint32_t)(uintptr_t)(lds_void*)smem;
+    lane = tid & 63;
+    wave = tid >> 6;
+    s = lane & 15;
+    g = lane >> 4;
+    m = (blk * P::WAVES + wave) * 16 + s;
+    wb32 = blk * (P::WAVES / 2) + (wave >> 1);
+    const uint32_t sb = 16u * (uint32_t)(wave & 1) + (uint32_t)s;
+    lold = sb + 32u * (uint32_t)(g & 1);
+    st_off = 16u * lold + 8u * (uint32_t)(g >> 1);
+    gsh = 2u * (uint32_t)(g >> 1);
+    one16 = opaque_one16();
+    dl = DmaLean{a.wpack, (uint32_t)(lane * 16 + wave * 1024),
+                 (uint32_t)__builtin_amdgcn_readfirstlane(lds_base + (uint32_t)wave * 1024u),
+                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)wave)};
+  }
+
+  template <int gi> __device__ __forceinline__ void fetch() {
+    constexpr Group G = GT::t.g[gi];
+    fetch_group_lean<P, G.c0, G.nch, (gi % NSLOT) * SLOT_CAP * 1024>(dl);
+  }
+  template <int gi, int i> __device__ __forceinline__ void fetch_piece() {
+    constexpr Group G = GT::t.g[gi];
+    fetch_piece_lean<P, G.c0, G.nch, (gi % NSLOT) * SLOT_CAP * 1024, i>(dl);
+  }
+  template <int S> __device__ __forceinline__ Tile& slot() {
+    if constexpr (S >= TS_HA && S < TS_HB) return Ha[S - TS_HA];
+    else if constexpr (S >= TS_HB && S < TS_X) return Hb[S - TS_HB];
+    else if constexpr (S == TS_X || S == TS_X + 1) return X[S - TS_X];
+    else {
+      static_assert(S == TS_D, "forward tile slot");
+      return D;
+    }
+  }
+  template <int u> static __host__ __device__ constexpr int layer_of() { return fwd16_unit_layer(u); }
+  template <int u> static __host__ __device__ constexpr int tile_of() { return u - fwd16_unit_first(fwd16_unit_layer(u)); }
+
+  // vector-memory stores issued by unit u's finish
+  static __host__ __device__ constexpr int unit_stores(int u) {
+    if (!STORE) return 0;
+    const int L = fwd16_unit_layer(u), mt = u - fwd16_unit_first(L);
+    if (L == LFA) return mt < 16 ? SST : 0;
+    if (L == LRGB) return 0;
+    return SST + (mt == fwd16_out_tiles(L) - 1 ? 1 : 0);  // + the layer's mask store
+  }
+  static __host__ __device__ constexpr int group_stores(int gi) {
+    int n = 0;
+    for (int u = 0; u < NUNIT_FWD16; ++u)
+      if (finished_in_group<2, DENSITY, P::CH, cross_finish<P, 2>()>(gi, u)) n += unit_stores(u);
+    return n;
+  }
+  // the training stores of one 32-feature tile (a K-block, or the two 16-row tiles that fill it): old
+  // tile tau, 8 bytes of chunk c (hi) [and c + 2 (lo)] at this lane's slot
+  __device__ __forceinline__ void store_half(int tau, int c, uint32_t h0, uint32_t h1, uint32_t l0, uint32_t l1) {
+    char* base = (char*)a.act + (((wb32 * AT_TILES + tau) * SCH + c) << 10) + st_off;
+    store8(base, h0, h1);
+    if constexpr (!HALF) store8(base + 2048, l0, l1);
+  }
+  __device__ __forceinline__ void store_kblock(int tau, const Tile& t) {
+    store_half(tau, 0, get_dword(t.hi, 0), get_dword(t.hi, 1), get_dword(t.lo, 0), get_dword(t.lo, 1));
+    store_half(tau, 1, get_dword(t.hi, 2), get_dword(t.hi, 3), get_dword(t.lo, 2), get_dword(t.lo, 3));
+  }
+
+  // ---- group_body hooks
+  template <int u> static __host__ __device__ constexpr int group_of() {
+    int gi = 0;
+    while (!(GT::t.g[gi].u0 <= u && u < GT::t.g[gi].u0 + GT::t.g[gi].n)) ++gi;
+    return gi;
+  }
+  template <int u, int t> __device__ __forceinline__ const Tile& in_tile() {
+    return slot<fwd_in_slot(layer_of<u>(), t)>();
+  }
+  // the unit's bias chunk (rows 4 g + {0..3} = lane g) is the MFMA chain's initial accumulator, read one unit ahead
+  template <int u> __device__ __forceinline__ void prefetch() {
+    constexpr int BOFF = unit_chunk_off<2>(u, CH) - GT::t.g[group_of<u>()].c0 + fwd_in_tiles(layer_of<u>()) * CH;
+    bias = as_uint4(wbg[BOFF * 64]);
+  }
+  template <int u> __device__ __forceinline__ void init(Acc& acc) {
+    constexpr int L = layer_of<u>(), mt = tile_of<u>();
+    if constexpr (L == L5 && mt == 0 && !keep_pe<P>()) {
+      settle(px);
+      settle(py);
+      settle(pz);
+      pe_kblock<0, 10, 63>(X[0], g, px, py, pz);
+      pe_kblock<1, 10, 63>(X[1], g, px, py, pz);
+    }
+    if constexpr (L == LV && mt == 0) {
+      settle(dx);
+      settle(dy);
+      settle(dz);
+      pe_kblock<0, 4, 27>(D, g, dx, dy, dz);
+    }
+    acc[0] = __uint_as_float(bias.x);
+    acc[1] = __uint_as_float(bias.y);
+    acc[2] = __uint_as_float(bias.z);
+    acc[3] = __uint_as_float(bias.w);
+  }
+  // part p of NP of output tile mt's finish: its register pairs [2p/NP, 2(p+1)/NP) into half mt & 1 of the
+  // output K-block (in place), their mask bits; the last part stores (and the layer's last tile the masks)
+  template <int u, int p> __device__ __forceinline__ void finish_part(const Acc& acc) {
+    constexpr int L = layer_of<u>(), mt = tile_of<u>();
+    constexpr int NP = finish_parts<P>();
+    constexpr int K0 = 2 * p / NP, K1 = 2 * (p + 1) / NP;
+    constexpr bool LASTP = p == NP - 1;
+    if constexpr (L <= L7 || L == LV || (L == LFA && mt < 16)) {
+      constexpr bool RELU = L != LFA;  // feature_linear: no activation
+      constexpr int Q = 2 * (mt & 1);   // the K-block dwords of this tile: Q, Q + 1
+      Tile& out = slot<fwd_out_slot(L, mt >> 1)>();
+      uint32_t bits = 0;
+      sfor<K1 - K0>([&](auto kk) {
+        constexpr int k = K0 + decltype(kk)::value;
+        float y0 = acc[2 * k], y1 = acc[2 * k + 1];
+        if constexpr (RELU) {
+          y0 = __int_as_float(max(__float_as_int(y0), 0));
+          y1 = __int_as_float(max(__float_as_int(y1), 0));
+        }
+        const uint32_t hw = pack_bf16(y0, y1);
+        const uint32_t lw = pack_bf16(y0 - __uint_as_float(hw << 16), y1 - __uint_as_float(hw & 0xffff0000u));
+        if constexpr (STORE && RELU) bits |= nonzero_bf16x2(hw, one16) << k;  // bits k / 16 + k (as PBF3)
+        set_dword8(out.hi, Q + k, hw);
+        set_dword8(out.lo, Q + k, lw);
+      });
+      if constexpr (STORE) {
+        constexpr int n = mt >> 1, d = mt >> 2;  // old 32-row tile, its mask dword
+        if constexpr (RELU) {
+          // value 2k + j of this lane = old register rho = 4 (2 (mt & 1) + (g >> 1)) + 2k + j of old tile n, old
+          // lane half h = g & 1: mask bit 8 (n & 1) + (rho >> 1) + 16 (rho & 1) = [bit k / 16 + k] << (C + gsh)
+          constexpr uint32_t C = 8 * (n & 1) + 4 * (mt & 1);
+          const uint32_t b = bits << (C + gsh);
+          if constexpr ((mt & 3) == 0 && p == 0) mw[d] = b;
+          else mw[d] |= b;
+        }
+        if constexpr (LASTP) {
+          constexpr int tau = (L == LV ? AT_V : L == LFA ? AT_F : AT_H + 8 * L) + n;
+          store_half(tau, mt & 1, get_dword(out.hi, Q), get_dword(out.hi, Q + 1), get_dword(out.lo, Q),
+                     get_dword(out.lo, Q + 1));
+          if constexpr (RELU && mt == fwd16_out_tiles(L) - 1) {
+            // old lane L gets its bits from lanes l and l + 32 (g = h, h + 2): OR in the partner's dwords; lanes l
+            // and l + 32 then hold the same 16 bytes for the same old lane and both store them
+            constexpr int ND = L == LV ? 2 : 4;
+            uint32_t full[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int q = 0; q < ND; ++q) {
+              const auto r = __builtin_amdgcn_permlane32_swap(mw[q], mw[q], false, false);
+              full[q] = mw[q] | (lane < 32 ? r[1] : r[0]);
+            }
+            store16<0>((uint4*)((char*)a.masks + ((wb32 * MASK_GROUPS + (L == LV ? 8 : L)) * 64 + lold) * 16),
+                       make_uint4(full[0], full[1], full[2], full[3]));
+          }
+        }
+      }
+    } else if constexpr (L == LFA) {  // the alpha row: row 0 = register 0 of lane group 0
+      if constexpr (p == 0) alpha = acc[0];
+    } else if constexpr (p == 0) {    // LRGB: rows 0..2 = registers 0..2 of lane group 0
+      rgb0 = acc[0];
+      rgb1 = acc[1];
+      rgb2 = acc[2];
+    }
+  }
+
+  template <int gi> __device__ __forceinline__ void step() {
+    constexpr int NG = GT::t.n;
+    if constexpr (gi + PF < NG && dma_spread<P>() == 0) fetch<gi + PF>();
+    const uint32_t sl = lds_base + (uint32_t)((gi % NSLOT) * SLOT_CAP * 1024);
+    wbg = lds_ptr(sl + (uint32_t)(g * 16));
+    group_body<P, 2, DENSITY, gi>(*this, lds_ptr(sl + (uint32_t)(lane * 16)));
+    constexpr int N = dma_spread<P>() > 0
+        ? handoff_vmcnt_spread<P, 2, DENSITY>(gi, [](int u) constexpr { return unit_stores(u); })
+        : handoff_vmcnt<P, 2, DENSITY>(gi, [](int i) constexpr { return group_stores(i); }, STORE ? 6 * SST : 0);
+    if constexpr (gi + 1 < NG) wait_barrier<N>();
+  }
+
+  __device__ __forceinline__ void run() {
+    const int64_t ms = m < a.M ? m : a.M - 1;
+    px = a.pts[ms * 3 + 0];
+    py = a.pts[ms * 3 + 1];
+    pz = a.pts[ms * 3 + 2];
+    dx = dy = dz = 0.f;
+    if constexpr (!DENSITY) {
+      const int64_t di = a.dir_index ? (int64_t)a.dir_index[ms] : ms / a.samples_per_dir;
+      dx = a.dirs[di * 3 + 0];
+      dy = a.dirs[di * 3 + 1];
+      dz = a.dirs[di * 3 + 2];
+    }
+    sfor<(PF < GT::t.n ? PF : GT::t.n)>([&](auto gg) { fetch<decltype(gg)::value>(); });
+    pe_kblock<0, 10, 63>(X[0], g, px, py, pz);
+    pe_kblock<1, 10, 63>(X[1], g, px, py, pz);
+    if constexpr (STORE) {
+      Tile Dt;
+      pe_kblock<0, 4, 27>(Dt, g, dx, dy, dz);
+      store_kblock(AT_X, X[0]);
+      store_kblock(AT_X + 1, X[1]);
+      store_kblock(AT_D, Dt);
+    }
+    {  // group 0 landed: younger = the DMAs of groups 1 .. PF - 1 and the PE stores (3 K-blocks x 2 halves)
+      constexpr int N0 = [] {
+        int n = STORE ? 6 * SST : 0;
+        for (int j = 1; j < PF && j < GT::t.n; ++j) n += group_dma<P, 2, DENSITY>(j);
+        return n;
+      }();
+      wait_barrier<N0>();
+    }
+    settle(dx);
+    settle(dy);
+    settle(dz);
+    sfor<GT::t.n>([&](auto gg) { step<decltype(gg)::value>(); });
+    if (g == 0 && m < a.M)
+      *(float4*)(a.raw + m * 4) = DENSITY ? make_float4(0.f, 0.f, 0.f, alpha) : make_float4(rgb0, rgb1, rgb2, alpha);
+  }
+};
+
+template <class P, bool STORE, bool DENSITY, bool PERSIST, bool HALF>
+using FwdWaveOf = std::conditional_t<P::KIND == K_BF16X3W, FwdWave16<STORE, DENSITY, PERSIST, HALF>,
+                                     FwdWave<P, STORE, DENSITY, PERSIST, HALF>>;
+
 // PERSIST (inference only): the sample count is read on the device (a.M_dev, e.g. the grid
 // march's gather count: no host round trip sizes the launch) and a grid of one wave of
 // workgroups loops over the sample blocks; the barrier at the end of each block keeps the next
@@ -1510,7 +1949,7 @@ template <class P, bool STORE, bool DENSITY, bool PERSIST, bool HALF = false>
 __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
   if constexpr (!PERSIST) {
-    FwdWave<P, STORE, DENSITY, false, HALF> w(a, smem_u4, blockIdx.x, threadIdx.x);
+    FwdWaveOf<P, STORE, DENSITY, false, HALF> w(a, smem_u4, blockIdx.x, threadIdx.x);
     w.run();
   } else {
     static_assert(!STORE, "the persistent forward is inference only");
@@ -1523,7 +1962,7 @@ __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
       // instead of being hoisted out of the loop and held in registers across it (spills)
       int tid = threadIdx.x;
       asm volatile("" : "+v"(tid));
-      FwdWave<P, STORE, DENSITY, true> w(b, smem_u4, blk, tid);
+      FwdWaveOf<P, STORE, DENSITY, true, false> w(b, smem_u4, blk, tid);
       w.run();
       __syncthreads();
     }
@@ -2426,34 +2865,56 @@ static void launch_fwd_any(const FwdArgs& a, bool store, bool density, hipStream
 // unit (no NERF_MLP_PREC) only declares them, so the three precisions compile in parallel.
 namespace nerf {
 namespace mlp {
-// the pack plan of (P, dir) on the current device: built on first use (one launch, then a stream sync),
-// kept for the process; null if it cannot be allocated (the caller falls back to pack_kernel)
+// the pack plan of (P, dir) on the device that holds the parameters: built on first use (one launch, then a
+// stream sync), kept for the process; null if it cannot be allocated, or while the stream is being captured
+// (the build syncs), and the caller falls back to pack_kernel.  The device comes from the parameter pointer,
+// not the current device (a net on cuda:1 packed while cuda:0 is current), and the build runs under a device
+// guard on that device.  (round 6)
+static_assert(NET_PARAMS < (1 << 24), "a plan entry holds a 24-bit parameter offset");
+// the packed-weight layout of a policy's forward: 32-row units (0), or the 16-row units of PBF3W (2)
+template <class P> static constexpr int fwd_layout() { return P::KIND == K_BF16X3W ? 2 : 0; }
+template <class P, class F> static void with_layout(int dir, F&& f) {  // f(integral_constant<layout>)
+  if (dir == 1) {
+    if constexpr (fwd_layout<P>() != 2) f(std::integral_constant<int, 1>{});  // (PBF3W: forward only)
+  } else {
+    f(std::integral_constant<int, fwd_layout<P>()>{});
+  }
+}
 template <class P>
-static const uint32_t* pack_plan(int dir, hipStream_t stream) {
+static const uint32_t* pack_plan(int dir, const void* params, hipStream_t stream) {
   static std::mutex mu;
   static uint32_t* plans[64][2] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, params) != hipSuccess || at.device < 0 || at.device >= 64) return nullptr;
+  const int dev = at.device;
   std::lock_guard<std::mutex> lock(mu);
   uint32_t*& plan = plans[dev][dir];
   if (!plan) {
-    const int64_t n = total_chunks(P::CH, dir) * 64;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || (cur != dev && hipSetDevice(dev) != hipSuccess)) return nullptr;
+    const int64_t n = total_chunks(P::CH, dir == 0 ? fwd_layout<P>() : 1) * 64;
     uint32_t* p = nullptr;
-    if (hipMalloc(&p, (size_t)n * P::E * sizeof(uint32_t)) != hipSuccess) return nullptr;
-    dim3 grid((unsigned)((n + 255) / 256));
-    if (dir == 0) hipLaunchKernelGGL((pack_plan_kernel<P, 0>), grid, dim3(256), 0, stream, unit_offsets<P::CH, 0>(), p);
-    else hipLaunchKernelGGL((pack_plan_kernel<P, 1>), grid, dim3(256), 0, stream, unit_offsets<P::CH, 1>(), p);
-    if (hipStreamSynchronize(stream) != hipSuccess) {
-      (void)hipFree(p);
-      return nullptr;
+    bool ok = hipMalloc(&p, (size_t)n * P::E * sizeof(uint32_t)) == hipSuccess;
+    if (ok) {
+      dim3 grid((unsigned)((n + 255) / 256));
+      with_layout<P>(dir, [&](auto lay) {
+        constexpr int D = decltype(lay)::value;
+        hipLaunchKernelGGL((pack_plan_kernel<P, D>), grid, dim3(256), 0, stream, unit_offsets<P::CH, D>(), p);
+      });
+      ok = hipStreamSynchronize(stream) == hipSuccess;
+      if (!ok) (void)hipFree(p);
     }
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!ok) return nullptr;
     plan = p;
   }
   return plan;
 }
 template <class P>
 void mlp_pack_impl(const ParamPtrs& prm, int dir, char* dst, hipStream_t stream) {
-  const int64_t n = total_chunks(P::CH, dir) * 64;
+  const int64_t n = total_chunks(P::CH, dir == 0 ? fwd_layout<P>() : 1) * 64;
   dim3 grid((unsigned)((n + 255) / 256));
   // the 24 parameters back to back (FusedAdam's flat buffer): the plan gather (NERF_PACK_PLAN=0: always
   // the direct pack, for A/B timing)
@@ -2461,22 +2922,31 @@ void mlp_pack_impl(const ParamPtrs& prm, int dir, char* dst, hipStream_t stream)
   bool flat = !(env && env[0] == '0');
   for (int k = 1; k < NPARAM; ++k) flat = flat && prm.p[k] == prm.p[0] + param_offset(k);
   if (flat) {
-    if (const uint32_t* plan = pack_plan<P>(dir, stream)) {
+    if (const uint32_t* plan = pack_plan<P>(dir, prm.p[0], stream)) {
       hipLaunchKernelGGL((pack_gather_kernel<P>), grid, dim3(256), 0, stream, prm.p[0], plan, dst, n);
       return;
     }
   }
-  if (dir == 0) hipLaunchKernelGGL((pack_kernel<P, 0>), grid, dim3(256), 0, stream, prm, unit_offsets<P::CH, 0>(), dst);
-  else hipLaunchKernelGGL((pack_kernel<P, 1>), grid, dim3(256), 0, stream, prm, unit_offsets<P::CH, 1>(), dst);
+  with_layout<P>(dir, [&](auto lay) {
+    constexpr int D = decltype(lay)::value;
+    hipLaunchKernelGGL((pack_kernel<P, D>), grid, dim3(256), 0, stream, prm, unit_offsets<P::CH, D>(), dst);
+  });
 }
 template <class P>
 void mlp_fwd_train_impl(const FwdArgs& a, hipStream_t stream) {
   launch_fwd<P, true, false>(a, stream);
 }
+// The bf16x3 forward (training, bf16x3f training with bf16 stores, inference, density, persistent): the wide
+// 16x16x32 kernel (PBF3W, round 6) or, with -DNERF_BF3_WIDE=0, the 32x32x16 one (PBF3) for A/B builds.  The
+// bf16x3 backward (dX / dW, and its W^T pack) is PBF3's either way: both forwards write the same stores.
+#ifndef NERF_BF3_WIDE
+#define NERF_BF3_WIDE 1
+#endif
+using PBF3F = std::conditional_t<NERF_BF3_WIDE != 0, PBF3W, PBF3>;
 // bf16x3 forward, bf16 (hi-half) stores for the bf16 backward
 void mlp_fwd_train_half_impl(const FwdArgs& a, hipStream_t stream);
 #if defined(NERF_MLP_PREC) && NERF_MLP_PREC == 2 && (!defined(NERF_MLP_PART) || NERF_MLP_PART == 4)
-void mlp_fwd_train_half_impl(const FwdArgs& a, hipStream_t stream) { launch_fwd<PBF3, true, false, true>(a, stream); }
+void mlp_fwd_train_half_impl(const FwdArgs& a, hipStream_t stream) { launch_fwd<PBF3F, true, false, true>(a, stream); }
 #endif
 // the three inference forwards, one translation unit each (parts 1, 5, 6)
 template <class P>
@@ -2513,10 +2983,18 @@ void mlp_dw_impl(const DwArgs& w, dim3 grid, hipStream_t stream) {
 #define NERF_MLP_IMPLS(EXT, P) \
   NERF_MLP_I_PACK(EXT, P) NERF_MLP_I_FWDT(EXT, P) NERF_MLP_I_FWDI(EXT, P) NERF_MLP_I_FWDD(EXT, P) \
   NERF_MLP_I_FWDP(EXT, P) NERF_MLP_I_DX(EXT, P) NERF_MLP_I_DW(EXT, P)
+#define NERF_MLP_FWDS(EXT, P) \
+  NERF_MLP_I_FWDT(EXT, P) NERF_MLP_I_FWDI(EXT, P) NERF_MLP_I_FWDD(EXT, P) NERF_MLP_I_FWDP(EXT, P)
 #if !defined(NERF_MLP_PREC)
 NERF_MLP_IMPLS(extern, PF32)
 NERF_MLP_IMPLS(extern, PBF16)
-NERF_MLP_IMPLS(extern, PBF3)
+NERF_MLP_I_PACK(extern, PBF3)  // bf16x3: the W^T pack, dX, dW (+ the forward pack when not wide)
+NERF_MLP_I_DX(extern, PBF3)
+NERF_MLP_I_DW(extern, PBF3)
+NERF_MLP_FWDS(extern, PBF3F)
+#if NERF_BF3_WIDE
+NERF_MLP_I_PACK(extern, PBF3W)
+#endif
 NERF_MLP_I_FWDI(extern, PBF6)  // bf16x6: the inference forward and its pack only
 NERF_MLP_I_PACK(extern, PBF6)
 #elif NERF_MLP_PREC == 3
@@ -2534,21 +3012,29 @@ NERF_MLP_I_PACK(, PBF6)
 #else
 #define NERF_PP PBF3
 #endif
+#if NERF_MLP_PREC == 2
+#define NERF_PP_FWD PBF3F  // (the bf16x3 forwards: PBF3W unless NERF_BF3_WIDE=0)
+#else
+#define NERF_PP_FWD NERF_PP
+#endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 0
-NERF_MLP_I_FWDT(, NERF_PP)
+NERF_MLP_I_FWDT(, NERF_PP_FWD)
 #endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 1
-NERF_MLP_I_FWDI(, NERF_PP)
+NERF_MLP_I_FWDI(, NERF_PP_FWD)
 #endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 5
-NERF_MLP_I_FWDD(, NERF_PP)
+NERF_MLP_I_FWDD(, NERF_PP_FWD)
 #endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 6
-NERF_MLP_I_FWDP(, NERF_PP)
+NERF_MLP_I_FWDP(, NERF_PP_FWD)
 #endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 2
 NERF_MLP_I_DX(, NERF_PP)
 NERF_MLP_I_PACK(, NERF_PP)
+#if NERF_MLP_PREC == 2 && NERF_BF3_WIDE
+NERF_MLP_I_PACK(, PBF3W)
+#endif
 #endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 3
 NERF_MLP_I_DW(, NERF_PP)
@@ -2576,6 +3062,7 @@ int64_t nerf_mlp_packed_bytes(int dtype, int dir) {
   if (dtype == 4) return dir == 0 ? total_chunks(PBF6::CH, 0) * 1024 : -1;
   if (!train_dtype(dtype) || (dir != 0 && dir != 1)) return -1;
   const int p = dir == 0 ? fwd_prec(dtype) : bwd_prec(dtype);
+  if (p == 2 && dir == 0) return total_chunks(PBF3F::CH, fwd_layout<PBF3F>()) * 1024;  // (the wide bf16x3 forward)
   return total_chunks(p == 1 ? PBF16::CH : PF32::CH, dir) * 1024;  // bf16x3: CH 4 as fp32
 }
 
@@ -2607,6 +3094,7 @@ int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void*
     if (p == 4) mlp_pack_impl<PBF6>(prm, dir, (char*)dst, stream);
     else if (p == 0) mlp_pack_impl<PF32>(prm, dir, (char*)dst, stream);
     else if (p == 1) mlp_pack_impl<PBF16>(prm, dir, (char*)dst, stream);
+    else if (dir == 0) mlp_pack_impl<PBF3F>(prm, dir, (char*)dst, stream);
     else mlp_pack_impl<PBF3>(prm, dir, (char*)dst, stream);
     if (int e = check_launch("nerf_mlp_pack")) return e;
   }
@@ -2632,13 +3120,13 @@ int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const floa
   if (store) {
     if (dtype == 0) mlp_fwd_train_impl<PF32>(a, stream);
     else if (dtype == 1) mlp_fwd_train_impl<PBF16>(a, stream);
-    else if (dtype == 2) mlp_fwd_train_impl<PBF3>(a, stream);
+    else if (dtype == 2) mlp_fwd_train_impl<PBF3F>(a, stream);
     else mlp_fwd_train_half_impl(a, stream);
   } else {
     if (dtype == 4) mlp_fwd_plain_impl<PBF6>(a, stream);
     else if (dtype == 0) mlp_fwd_infer_impl<PF32>(a, density, stream);
     else if (dtype == 1) mlp_fwd_infer_impl<PBF16>(a, density, stream);
-    else mlp_fwd_infer_impl<PBF3>(a, density, stream);
+    else mlp_fwd_infer_impl<PBF3F>(a, density, stream);
   }
   return check_launch("nerf_mlp_fwd");
 }
@@ -2656,7 +3144,7 @@ int nerf_mlp_fwd_count(const void* packed_fwd, int dtype, const float* pts, cons
             M_dev, M_cap};
   if (dtype == 0) mlp_fwd_infer_impl<PF32>(a, false, stream);
   else if (dtype == 1) mlp_fwd_infer_impl<PBF16>(a, false, stream);
-  else mlp_fwd_infer_impl<PBF3>(a, false, stream);
+  else mlp_fwd_infer_impl<PBF3F>(a, false, stream);
   return check_launch("nerf_mlp_fwd_count");
 }
 

@@ -127,6 +127,45 @@ __host__ __device__ constexpr int bwd_unit_tile_off(int u) {
 }
 constexpr int BWD_TILES = bwd_unit_tile_off(NUNIT_BWD);
 
+// 16-row forward units (round 6: the bf16x3 forward on v_mfma_f32_16x16x32_bf16, 16 samples per
+// wave, two waves per SIMD).  Unit = one 16-row output tile of one layer; its input is the same
+// list of 32-feature K-blocks as the 32-row forward's input tiles.  B operand of K-block t: lane
+// l = s + 16 g (sample s, lane group g) holds 8 features, element e -> feature 32 t + k16_feat(g, e);
+// a 16x16 accumulator holds rows 4 g + {0..3} of sample s, so output tiles 2t and 2t + 1 ARE the
+// next layer's K-block t (elements 0..3 and 4..7) in registers, the weights permuted to match.
+__host__ __device__ constexpr int k16_feat(int g, int e) { return e < 4 ? 4 * g + e : 16 + 4 * g + (e - 4); }
+__host__ __device__ constexpr int fwd16_out_tiles(int L) {
+  return L == LFA ? 17 : L == LV ? 8 : L == LRGB ? 1 : 16;  // (LFA: 16 feature tiles + the alpha row)
+}
+constexpr int NUNIT_FWD16 = 8 * 16 + 17 + 8 + 1;  // 154
+__host__ __device__ constexpr int fwd16_unit_first(int L) {
+  int u = 0;
+  for (int k = 0; k < L; ++k) u += fwd16_out_tiles(k);
+  return u;
+}
+__host__ __device__ constexpr int fwd16_unit_layer(int u) {
+  int L = 0;
+  while (L < NLAYER - 1 && u >= fwd16_unit_first(L + 1)) ++L;
+  return L;
+}
+__host__ __device__ constexpr int fwd16_unit_tiles(int u) { return fwd_in_tiles(fwd16_unit_layer(u)); }
+__host__ __device__ constexpr int fwd16_unit_tile_off(int u) {  // in input K-blocks
+  int o = 0;
+  for (int k = 0; k < u; ++k) o += fwd16_unit_tiles(k);
+  return o;
+}
+constexpr int FWD16_TILES = fwd16_unit_tile_off(NUNIT_FWD16);
+// output tile m of layer L -> weight param, first weight row, valid rows
+__host__ __device__ constexpr int fwd16_out_weight(int L, int m) {
+  return L <= L7 ? 2 * L : L == LFA ? (m < 16 ? (int)P_FW : (int)P_AW) : L == LV ? (int)P_VW : (int)P_RW;
+}
+__host__ __device__ constexpr int fwd16_out_row0(int L, int m) { return (L == LFA && m == 16) ? 0 : 16 * m; }
+__host__ __device__ constexpr int fwd16_out_valid(int L, int m) {
+  return (L == LFA && m == 16) ? 1 : L == LRGB ? 3 : 16;
+}
+constexpr int NUNIT_MAX = NUNIT_FWD16;  // the largest unit table (forward 78, dX 76, 16-row forward 154)
+static_assert(NUNIT_FWD16 > NUNIT_FWD && NUNIT_FWD16 > NUNIT_BWD, "NUNIT_MAX");
+
 // Training stores, "fragment-native": a stored tensor is a list of 32-feature tiles; tile
 // tau of 32-sample block b occupies one tile-block of CH KiB at ((tau * nblk + b) * CH + c)
 // KiB (chunk c = accumulator registers [c*E, c*E+E) of every lane, lane-linear, 16 B per

@@ -47,7 +47,7 @@ def test_mlp_kernels_handoffs_and_registers(capsys):
                 or (persist and int(m.group(1)) <= 320)), "\n" + out
     assert re.search(r"ok  _ZN4nerf3mlp10fwd_kernelINS0_5PBF16ELb0ELb0ELb1E", out), "\n" + out
     for name in ("fwd_kernelINS0_5PBF16ELb1ELb0", "fwd_kernelINS0_4PF32ELb1ELb0", "dx_kernelINS0_4PF32",
-                 "fwd_kernelINS0_4PBF3ELb1ELb0ELb0ELb0E", "dx_kernelINS0_4PBF3", "dx_kernelINS0_5PBF16",
-                 "fwd_kernelINS0_4PBF3ELb1ELb0ELb0ELb1E", "fwd_kernelINS0_4PBF6ELb0ELb0ELb0E",
-                 "fwd_kernelINS0_4PBF3ELb0ELb1ELb0ELb0E", "fwd_kernelINS0_4PF32ELb0ELb0ELb1ELb0E"):
+                 "fwd_kernelINS0_5PBF3WELb1ELb0ELb0ELb0E", "dx_kernelINS0_4PBF3", "dx_kernelINS0_5PBF16",
+                 "fwd_kernelINS0_5PBF3WELb1ELb0ELb0ELb1E", "fwd_kernelINS0_4PBF6ELb0ELb0ELb0E",
+                 "fwd_kernelINS0_5PBF3WELb0ELb1ELb0ELb0E", "fwd_kernelINS0_4PF32ELb0ELb0ELb1ELb0E"):
         assert re.search(name + r".*counted_waits=\d+ unsafe=0", out), "\n" + out

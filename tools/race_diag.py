@@ -84,12 +84,20 @@ def main():
             torch.cuda.synchronize()
             fw.append((raw, act, masks))
         if ref is None:
-            ref = {"raw": fw[0][0], "masks": fw[0][2]}
+            ref = {"raw": fw[0][0], "masks": fw[0][2], "act": fw[0][1]}
         rec = {"raw_same_runs": all(torch.equal(f[0], fw[0][0]) for f in fw),
                "act_same_runs": all(torch.equal(f[1], fw[0][1]) for f in fw),
                "masks_same_runs": all(torch.equal(f[2], fw[0][2]) for f in fw),
                "raw_equal_first_build": bool(torch.equal(fw[0][0], ref["raw"])),
-               "raw_max_abs_diff_first_build": float((fw[0][0] - ref["raw"]).abs().max())}
+               "raw_max_abs_diff_first_build": float((fw[0][0] - ref["raw"]).abs().max()),
+               "raw_max_rel_diff_first_build": float(((fw[0][0] - ref["raw"]).abs() /
+                                                      ref["raw"].abs().clamp_min(1e-3)).max()),
+               "act_bf16_differing_first_build": float((fw[0][1].view(torch.int16) != ref["act"].view(torch.int16))
+                                                       .float().mean()) if fw[0][1].numel() == ref["act"].numel()
+               else None,
+               "mask_bits_differing_first_build": float(
+                   (fw[0][2].view(torch.uint8) ^ ref["masks"].view(torch.uint8)).to(torch.int32).bitwise_and(255)
+                   .ne(0).float().mean())}
         mism = []
         for raw, act, masks in fw:
             exp = expected_masks(act, nblk)
