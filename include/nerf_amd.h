@@ -92,6 +92,17 @@ int nerf_composite_pdf(const float* raw, const float* z, const float* dirs, int 
                        int white_bkgd, float* rgb, float* depth, float* acc, float* weights, int Ni, int det,
                        const float* u_lin, const float* u, uint64_t seed, uint64_t offset, const float* rays,
                        float* z_fine, float* pts_fine, hipStream_t stream);
+/* (ABI 4) nerf_composite_pdf at det (u = u_lin, the linspace of volume_renderer.py:96-99) that also flags
+ * "fragile" rays: fragile[r] = 1 when an importance sample's bin (searchsorted) could change if every CDF entry c
+ * moved by up to rel_tol * min(c, 1 - c) + abs_tol, or the den of its interval is within den_tol of the
+ * den < 1e-5 switch (volume_renderer.py:120-126; den_tol 0: not flagged), or (z_tol > 0) those CDF moves
+ * could move a sample within its bin by more than z_tol -- the rays whose fine samples a slightly different
+ * coarse MLP could move.  The render of the split-bf16 tiers evaluates its coarse net in the tier's own arithmetic and
+ * re-evaluates only these rays at fp32 (Renderer.render). */
+int nerf_composite_pdf_fragile(const float* raw, const float* z, const float* dirs, int dir_stride, int64_t R, int Sc,
+                               int white_bkgd, float* rgb, float* depth, float* acc, int Ni, const float* u_lin,
+                               const float* rays, float* z_fine, float* pts_fine, float rel_tol, float abs_tol,
+                               float den_tol, float z_tol, int32_t* fragile, hipStream_t stream);
 
 /* ---- (a10) loss: MSE(rgb_map_c, gt) + MSE(rgb_map_f, gt) (src/train/trainers/nerf.py:21-29) -----
  * n = 3 R values.  fwd: out[3] = (loss_c, loss_f, loss_c + loss_f), one workgroup, fp64 sums in a

@@ -29,6 +29,6 @@ extern "C" {
 const char* nerf_last_error(void) { return nerf::g_last_error; }
 
 // bumped whenever an exported signature changes
-int nerf_abi_version(void) { return 3; }  // 3: dtype 3 (bf16x3f), nerf_composite_pdf, nerf_mse2_*
+int nerf_abi_version(void) { return 4; }  // 3: dtype 3 (bf16x3f), nerf_composite_pdf, nerf_mse2_*; 4: nerf_composite_pdf_fragile
 
 }  // extern "C"

@@ -217,6 +217,10 @@ struct PdfArgs {
   float* samples;        // [R, Ni] or null (unsorted, in u order)
   float* cdf_out;        // [R, Sc-1] or null
   int32_t* inds_out;     // [R, Ni] or null
+  // (round 6) per-ray "fragile" flag or null: 1 when some importance sample's bin, or the den < 1e-5 switch
+  // of its interval, could change if every CDF entry c moved by up to rel_tol min(c, 1 - c) + abs_tol
+  int32_t* fragile;
+  float rel_tol, abs_tol, den_tol, z_tol;
 };
 
 // one ray (one wave): zc = z of coarse sample l (l < Sc), wn = its weight of sample l + 1
@@ -239,6 +243,9 @@ __device__ __forceinline__ void sample_pdf_ray(const PdfArgs& a, int64_t r, int 
 
   float v[4];
   v[0] = l < a.Sc ? zc : __builtin_inff();
+  bool frag = false;
+  // the last two CDF entries (the u = 1 end case of the fragile flag)
+  const float c_last = __shfl(cdf, nb - 1, 64), c_prev = __shfl(cdf, nb > 1 ? nb - 2 : 0, 64);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int i = l + 64 * q;
@@ -254,14 +261,35 @@ __device__ __forceinline__ void sample_pdf_ray(const PdfArgs& a, int64_t r, int 
     const float cb = __shfl(cdf, below, 64), ca = __shfl(cdf, above, 64);
     const float bb = __shfl(bin, below, 64), ba = __shfl(bin, above, 64);
     if (i < a.Ni) {
-      float den = fsub(ca, cb);
-      den = den < 1e-5f ? 1.f : den;
+      const float den0 = fsub(ca, cb);
+      const float den = den0 < 1e-5f ? 1.f : den0;
       const float t = fdiv(fsub(u, cb), den);
       s = fadd(bb, fmul(t, fsub(ba, bb)));
       if (a.samples) a.samples[r * a.Ni + i] = s;
       if (a.inds_out) a.inds_out[r * a.Ni + i] = ind;
+      if (a.fragile) {
+        // the bin of u changes iff an entry crosses u: its neighbours cdf[ind - 1] <= u < cdf[ind] (cdf[0] = 0 is
+        // exact).  The last entry against u = 1 (the linspace's end) is its own case: with cdf[nb-1] <= 1 the
+        // sample is the last bin edge, with cdf[nb-1] > 1 it is that edge too -- unless the last interval's pdf
+        // is below the 1e-5 switch, when it drops to the start of that bin.  So that flip is flagged only when
+        // the last entry is within abs_tol of 1 and the last interval is below 1e-5 + den_tol.  The den < 1e-5
+        // switch (volume_renderer.py:124) elsewhere is flagged within den_tol of 1e-5
+        const bool end = u >= 1.f;
+        const float tb = fadd(fmul(a.rel_tol, fminf(cb, fsub(1.f, cb))), a.abs_tol);
+        const float ta = fadd(fmul(a.rel_tol, fminf(ca, fsub(1.f, ca))), a.abs_tol);
+        if (ind - 1 >= 1 && !(end && ind - 1 == nb - 1) && fsub(u, cb) < tb) frag = true;
+        if (ind <= nb - 1 && !(end && ind == nb - 1) && fsub(ca, u) <= ta) frag = true;
+        if (below != above && fabsf(fsub(den0, 1e-5f)) <= a.den_tol) frag = true;
+        if (end && fabsf(fsub(c_last, 1.f)) <= a.abs_tol && fsub(c_last, c_prev) < fadd(1e-5f, a.den_tol)) frag = true;
+        // within a bin the sample moves by (dcb + t ddcb) / den of the bin width: flag a move beyond z_tol
+        if (a.z_tol > 0.f && den0 >= 1e-5f && fmul(fdiv(fadd(ta, tb), den0), fsub(ba, bb)) > a.z_tol) frag = true;
+      }
     }
     v[1 + q] = s;
+  }
+  if (a.fragile) {
+    const bool any = __ballot(frag) != 0;
+    if (l == 0) a.fragile[r] = any ? 1 : 0;
   }
   v[3] = __builtin_inff();
   // positions >= Sc + Ni hold +inf; the first Sc+Ni sorted entries are the merged depths
@@ -599,6 +627,25 @@ int nerf_composite_pdf(const float* raw, const float* z, const float* dirs, int 
   PdfArgs p{z, nullptr, R, Sc, Ni, det, u_lin, u, seed, offset, rays, z_fine, pts_fine, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(composite_pdf_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, stream, c, p);
   return check_launch("nerf_composite_pdf");
+}
+
+int nerf_composite_pdf_fragile(const float* raw, const float* z, const float* dirs, int dir_stride, int64_t R, int Sc,
+                               int white_bkgd, float* rgb, float* depth, float* acc, int Ni, const float* u_lin,
+                               const float* rays, float* z_fine, float* pts_fine, float rel_tol, float abs_tol,
+                               float den_tol, float z_tol, int32_t* fragile, hipStream_t stream) {
+  NERF_REQUIRE(Sc >= 3 && Sc <= 64 && Ni >= 1 && Ni <= 128 && Sc + Ni <= 256 && R >= 0 && dir_stride >= 3,
+               "nerf_composite_pdf_fragile: need 3 <= Sc <= 64, 1 <= Ni <= 128 (got %d, %d)", Sc, Ni);
+  if (R == 0) return 0;
+  NERF_REQUIRE(raw && z && dirs && rgb && depth && acc && z_fine && u_lin && fragile,
+               "nerf_composite_pdf_fragile: null pointer");
+  NERF_REQUIRE(!pts_fine || rays, "nerf_composite_pdf_fragile: pts_fine needs rays");
+  NERF_REQUIRE(rel_tol >= 0.f && abs_tol >= 0.f && den_tol >= 0.f && z_tol >= 0.f,
+               "nerf_composite_pdf_fragile: negative tolerance");
+  CompArgs c{raw, z, dirs, dir_stride, R, Sc, white_bkgd, rgb, depth, acc, nullptr, nullptr, nullptr, nullptr, nullptr};
+  PdfArgs p{z, nullptr, R, Sc, Ni, 1, u_lin, nullptr, 0, 0, rays, z_fine, pts_fine, nullptr, nullptr, nullptr,
+            fragile, rel_tol, abs_tol, den_tol, z_tol};
+  hipLaunchKernelGGL(composite_pdf_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, stream, c, p);
+  return check_launch("nerf_composite_pdf_fragile");
 }
 
 int nerf_composite_bwd(const float* raw, const float* z, const float* dirs, int dir_stride, int64_t R, int S,

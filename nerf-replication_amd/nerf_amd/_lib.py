@@ -34,6 +34,8 @@ SIGNATURES = {
     "nerf_composite_bwd": (_i32, [_p, _p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _p]),
     "nerf_composite_pdf": (_i32, [_p, _p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _p, _i32, _i32, _p, _p, _u64, _u64,
                                   _p, _p, _p, _p]),
+    "nerf_composite_pdf_fragile": (_i32, [_p, _p, _p, _i32, _i64, _i32, _i32, _p, _p, _p, _i32, _p, _p, _p, _p, _f32,
+                                          _f32, _f32, _f32, _p, _p]),
     "nerf_mse2_fwd": (_i32, [_p, _p, _p, _i64, _p, _p]),
     "nerf_mse2_bwd": (_i32, [_p, _p, _p, _i64, _p, _p, _p, _p, _p, _p]),
     "nerf_mlp_net_params": (_i64, []),

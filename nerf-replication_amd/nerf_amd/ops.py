@@ -363,6 +363,38 @@ def composite_sample_pdf(raw: torch.Tensor, z: torch.Tensor, rays: torch.Tensor,
     return rgb, depth, acc, {"z_fine": z_fine, "pts_fine": pts_fine}
 
 
+@torch.no_grad()
+def composite_sample_pdf_fragile(raw: torch.Tensor, z: torch.Tensor, rays: torch.Tensor, white_bkgd: bool,
+                                 n_importance: int, rel_tol: float, abs_tol: float, den_tol: float = 0.0,
+                                 z_tol: float = 0.0):
+    """composite_sample_pdf at det (u = linspace), inference only, that also returns the per-ray fragile flag
+    (int32 [R]): 1 when an importance sample's bin could change if every CDF entry c moved by up to
+    rel_tol * min(c, 1 - c) + abs_tol, or the den of its interval is within den_tol of the den < 1e-5 switch, or
+    (z_tol > 0) those moves could shift a sample within its bin by more than z_tol (nerf_composite_pdf_fragile)."""
+    raw, z = _f32c(raw.reshape(z.shape[0], z.shape[1], 4), "raw"), _f32c(z, "z")
+    rays = _f32c(rays.reshape(-1, 6), "rays")
+    R, Sc = z.shape
+    dev = raw.device
+    keep, dptr, dstride = _dirs_view(rays[:, 3:6])
+    rgb = torch.empty(R, 3, device=dev, dtype=torch.float32)
+    depth = torch.empty(R, device=dev, dtype=torch.float32)
+    acc = torch.empty(R, device=dev, dtype=torch.float32)
+    S = Sc + n_importance
+    z_fine = torch.empty(R, S, device=dev, dtype=torch.float32)
+    pts_fine = torch.empty(R, S, 3, device=dev, dtype=torch.float32)
+    fragile = torch.empty(R, device=dev, dtype=torch.int32)
+    u_lin = device_table("linspace", 0.0, 1.0, n_importance, dev)
+    nbytes = R * (20 * Sc + 12 + 24 + 16 * S + 24)
+    with kernel_timer("composite_pdf", nbytes, detail=True):
+        check(lib().nerf_composite_pdf_fragile(ptr(raw), ptr(z), dptr, dstride, R, Sc, int(bool(white_bkgd)), ptr(rgb),
+                                               ptr(depth), ptr(acc), int(n_importance), ptr(u_lin), ptr(rays),
+                                               ptr(z_fine), ptr(pts_fine), float(rel_tol), float(abs_tol),
+                                               float(den_tol), float(z_tol), ptr(fragile), stream_of(raw)),
+              "nerf_composite_pdf_fragile")
+    del keep
+    return rgb, depth, acc, {"z_fine": z_fine, "pts_fine": pts_fine}, fragile
+
+
 class _Mse2(torch.autograd.Function):
     @staticmethod
     def forward(ctx, c, f, gt):

@@ -80,22 +80,29 @@ class Network(nn.Module):
         coarse pass every value of the frame holds the north_star's 2e-3 (tests/test_gpu_fullframe.py).
         The training forward (autograd) keeps bf16x3: at perturb 1 the importance samples are
         random draws from the CDF, which a 1e-5 relative perturbation leaves distributed the same.
-        task_arg.coarse_inference_dtype (default fp32) overrides the choice; "bf16x6" (operands
-        split exactly into three bf16, six products: fp32-class, faster than the fp32 MFMA) holds
-        2e-3 on the 4,096 sampled rays but leaves one frame pixel 2 uint8 levels off, so it is not
-        the default."""
+        task_arg.coarse_inference_dtype (default fp32) overrides the choice: "bf16x6" (operands split exactly
+        into three bf16, six products: fp32-class, faster than the fp32 MFMA) holds 2e-3 on the 4,096 sampled rays
+        but leaves one frame pixel 2 uint8 levels off; "selective" (round 6) is fp32 here, while Renderer.render
+        evaluates its coarse pass in the tier's arithmetic and re-evaluates at fp32 only the rays whose importance
+        samples a bounded CDF perturbation could move (nerf_composite_pdf_fragile) -- measured in round 6 to need
+        fp32 on 34-100 % of the frame's rays before it holds the frame's bounds (the samples move WITHIN their
+        bins by dcdf / den of a bin), so neither is the default."""
         dt = self.mlp_dtype
         if model != "fine" and dt in ("bf16x3", "bf16x3f"):
             recording = torch.is_grad_enabled() and any(p.requires_grad for p in fn.parameters())
             if not recording:
-                dt = cfg.task_arg.get("coarse_inference_dtype", "fp32") or dt
+                mode = cfg.task_arg.get("coarse_inference_dtype", "fp32") or dt
+                # "selective" (round 6, opt-in): Renderer.render's coarse pass runs the tier's own arithmetic and
+                # re-evaluates only the fragile rays at fp32 (passing dtype explicitly); any other caller of an
+                # inference coarse forward gets fp32, as with "fp32"
+                dt = "fp32" if mode == "selective" else mode
         return dt
 
-    def forward(self, inputs, viewdirs, model=""):
-        """inputs [R,S,3], viewdirs [R,3] -> raw [R,S,4] (network.py:171-192)."""
+    def forward(self, inputs, viewdirs, model="", dtype=None):
+        """inputs [R,S,3], viewdirs [R,3] -> raw [R,S,4] (network.py:171-192); dtype overrides the MLP arithmetic."""
         fn = self.model_fine if model == "fine" else self.model
         R, S = inputs.shape[0], inputs.shape[1]
-        raw = fn(inputs.reshape(-1, 3), viewdirs, S, None, self.mlp_dtype_for(model, fn))
+        raw = fn(inputs.reshape(-1, 3), viewdirs, S, None, dtype or self.mlp_dtype_for(model, fn))
         return raw.reshape(R, S, 4)
 
     def density(self, pts, model=""):

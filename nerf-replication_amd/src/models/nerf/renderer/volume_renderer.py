@@ -23,9 +23,20 @@ from nerf_amd import ops
 from src.config import cfg
 
 
+# fragile-ray tolerances of the (opt-in) selective coarse pass: a CDF entry c may move by FRAGILE_REL_TOL *
+# min(c, 1 - c) + FRAGILE_ABS_TOL between the split-bf16 and the fp32 coarse net; FRAGILE_Z_TOL > 0 also flags a
+# sample those moves could shift within its bin by more than it (tools/cdf_sensitivity.py, tools/selective_sweep.py,
+# holding the frame's bounds needed fp32 on 34-100 % of the rays)
+FRAGILE_REL_TOL = 1e-4
+FRAGILE_ABS_TOL = 1.2e-7
+FRAGILE_DEN_TOL = 0.0
+FRAGILE_Z_TOL = 0.0
+
+
 class Renderer:
     def __init__(self, net):
         self.net = net
+        self.fragile_rays = 0  # rays the selective coarse pass re-evaluated at fp32 (running count)
         self.occupancy_grid = None
         self.scene_bbox = None
         self.resolution = None
@@ -53,6 +64,12 @@ class Renderer:
         return ops.sample_pdf_bins(bins, weights, N_samples, det, seed=self._seed, offset=off)
 
     # ------------------------------------------------------------------ hierarchical render
+    def _selective(self, grad, perturb):
+        """The selective coarse pass (round 6, opt-in): an inference render (no autograd graph, perturb 0:
+        u = linspace) of a split-bf16 tier with task_arg.coarse_inference_dtype "selective"."""
+        return (not grad and not perturb and self.net.mlp_dtype in ("bf16x3", "bf16x3f")
+                and (cfg.task_arg.get("coarse_inference_dtype", "fp32") or "") == "selective")
+
     def _chunk(self, grad):
         ta = cfg.task_arg
         return int(ta.chunk_size) if grad else int(ta.get("render_chunk", ta.chunk_size))
@@ -97,12 +114,30 @@ class Renderer:
             else:
                 o1, o2 = self._next_offsets()
                 z, pts, vd = ops.sample_stratified(rc, near, far, n_s, perturb, seed=self._seed, offset=o1)
-            raw_c = self.net(pts, vd, "coarse")
             fused = n_i > 0 and float(ta.raw_noise_std) == 0.0 and n_s <= 64 and ta.get("fuse_composite_pdf", True)
-            if fused:  # raw2outputs + sample_pdf + merge in one launch (ops.composite_sample_pdf)
+            if fused and self._selective(grad, perturb):
+                # (round 6) the split-bf16 tiers' coarse pass in their own arithmetic; the fragile rays -- those
+                # whose importance samples a CDF perturbation of the coarse net's error could move across a bin
+                # (nerf_composite_pdf_fragile) -- re-evaluated at fp32, so that every ray's fine samples are the
+                # fp32 coarse net's (Network.mlp_dtype_for)
+                raw_c = self.net(pts, vd, "coarse", dtype=self.net.mlp_dtype)
+                rgb_c, dep_c, acc_c, pdf, frag = ops.composite_sample_pdf_fragile(
+                    raw_c, z, rc, white, n_i, float(ta.get("fragile_rel_tol", FRAGILE_REL_TOL)),
+                    float(ta.get("fragile_abs_tol", FRAGILE_ABS_TOL)), float(ta.get("fragile_den_tol", FRAGILE_DEN_TOL)),
+                    float(ta.get("fragile_z_tol", FRAGILE_Z_TOL)))
+                idx = frag.nonzero().squeeze(1)
+                self.fragile_rays += int(idx.numel())
+                if idx.numel():
+                    raw_x = self.net(pts[idx], vd[idx], "coarse", dtype="fp32")
+                    r2, d2, a2, p2 = ops.composite_sample_pdf(raw_x, z[idx], rc[idx], white, n_i, det=True)
+                    rgb_c[idx], dep_c[idx], acc_c[idx] = r2, d2, a2
+                    pdf["z_fine"][idx], pdf["pts_fine"][idx] = p2["z_fine"], p2["pts_fine"]
+            elif fused:  # raw2outputs + sample_pdf + merge in one launch (ops.composite_sample_pdf)
+                raw_c = self.net(pts, vd, "coarse")
                 rgb_c, dep_c, acc_c, pdf = ops.composite_sample_pdf(raw_c, z, rc, white, n_i, det=not perturb,
                                                                     seed=self._seed, offset=o2)
             else:
+                raw_c = self.net(pts, vd, "coarse")
                 rgb_c, dep_c, acc_c, w_c = self.raw2outputs(raw_c, z, rd, ta.raw_noise_std, white)
             ret = {"rgb_map_c": rgb_c, "depth_map_c": dep_c, "acc_map_c": acc_c}
             if n_i > 0:

@@ -39,7 +39,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_sizes_and_layout(lib):
-    assert lib.nerf_abi_version() == 3
+    assert lib.nerf_abi_version() == 4
     assert lib.nerf_mlp_net_params() == 595844
     # state_dict offsets: pts_linears.0.weight [256,63] then bias [256], ... rgb_linear.bias [3]
     assert lib.nerf_mlp_param_offset(0) == 0

@@ -144,6 +144,7 @@ def test_config2_full_frame_render(g4, frame, renderer, dtype):
     _compare(out, g4, "render", RENDER_KEYS, dtype)
 
 
+
 @pytest.mark.parametrize("dtype", TIERS)
 def test_config4_full_frame_march(g4, frame, renderer, dtype):
     """Config 4: the frame through render_accelerated on the reference's res-128 bake of the

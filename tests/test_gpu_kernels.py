@@ -915,6 +915,55 @@ def test_composite_pdf_fused_equals_separate(cuda, ops, det, Sc, Ni):
     assert torch.equal(raw.grad, raw2.grad)
 
 
+def test_composite_pdf_fragile_flag(cuda, ops):
+    """nerf_composite_pdf_fragile (round 6): its rgb / depth / acc / z_fine / pts_fine are composite_sample_pdf's
+    at det bit for bit, and its flag is exactly the documented rule, recomputed here from the CDF and the bins
+    (ops.sample_pdf debug outputs): some u = linspace(0, 1, Ni) within rel_tol * min(c, 1 - c) + abs_tol of a
+    bracketing entry c = cdf[k], k >= 1 (not the last entry against u = 1), or a den (cdf[above] - cdf[below],
+    below != above) within den_tol of the 1e-5 switch (volume_renderer.py:115-126), or u = 1 with the last entry
+    within abs_tol of 1 and the last interval below 1e-5 + den_tol."""
+    g = torch.Generator().manual_seed(77)
+    R, Sc, Ni = 2000, 64, 128
+    o = torch.randn(R, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, 4.0])
+    d = torch.nn.functional.normalize(torch.randn(R, 3, generator=g), dim=-1) * 1.3
+    rays = torch.cat([o, d], 1).to(cuda)
+    z, _, _ = ops.sample_stratified(rays, 2.0, 6.0, Sc, False)
+    raw = (torch.randn(R, Sc, 4, generator=g) * 2).to(cuda)
+    raw[: R // 2, :, 3] -= 6.0  # (half the rays nearly empty: CDF entries crowd near 0 / the 1e-5 switch)
+    rel, ab, dt = 1e-3, 1.2e-7, 2e-8
+    with torch.no_grad():
+        rgb, dep, acc, pdf = ops.composite_sample_pdf(raw, z, rays, True, Ni, det=True)
+        rgb2, dep2, acc2, pdf2, frag = ops.composite_sample_pdf_fragile(raw, z, rays, True, Ni, rel, ab, dt)
+        _, _, _, w = ops.composite(raw, z, rays[:, 3:6], True)
+        dbg = ops.sample_pdf(z, w, Ni, det=True, debug=True)
+    for a, b in ((rgb, rgb2), (dep, dep2), (acc, acc2), (pdf["z_fine"], pdf2["z_fine"]),
+                 (pdf["pts_fine"], pdf2["pts_fine"])):
+        assert torch.equal(a, b)
+    cdf, ind = dbg["cdf"].double().cpu(), dbg["inds"].long().cpu()
+    nb = Sc - 1
+    u = torch.linspace(0, 1, Ni, dtype=torch.float32).double()
+    tau = (rel * torch.minimum(cdf, 1 - cdf) + ab).float().double()
+    exp = torch.zeros(R, dtype=torch.bool)
+    for r in range(R):
+        for i in range(Ni):
+            k = int(ind[r, i])
+            end = u[i] >= 1.0
+            lo, hi = max(k - 1, 0), min(k, nb - 1)
+            if k - 1 >= 1 and not (end and k - 1 == nb - 1) and u[i] - cdf[r, k - 1] < tau[r, k - 1]:
+                exp[r] = True
+            if k <= nb - 1 and not (end and k == nb - 1) and cdf[r, k] - u[i] <= tau[r, k]:
+                exp[r] = True
+            if lo != hi and abs(float(torch.tensor(cdf[r, hi] - cdf[r, lo], dtype=torch.float32)) - 1e-5) <= dt:
+                exp[r] = True
+            if end and abs(float(cdf[r, nb - 1]) - 1.0) <= ab and \
+                    float(torch.tensor(cdf[r, nb - 1] - cdf[r, nb - 2], dtype=torch.float32)) < 1e-5 + dt:
+                exp[r] = True
+    got = frag.bool().cpu()
+    # (the kernel compares in fp32, this in fp64: allow the few rays whose margin equals the tolerance to the ulp)
+    assert int((got != exp).sum()) <= 2, (int(got.sum()), int(exp.sum()))
+    assert 0 < int(got.sum()) < R
+
+
 def test_mse_pair_matches_torch(cuda, ops):
     """ops.mse_pair = nn.MSELoss()(c, gt) + nn.MSELoss()(f, gt) (src/train/trainers/nerf.py:21-29):
     the losses within fp32 rounding of torch's (fp64 sums here), the gradients of the total (and of
