@@ -1701,7 +1701,11 @@ struct FwdWave16 {
   using Acc = f32x4;
   static constexpr int CH = P::CH;
   static constexpr int SCH = HALF ? 2 : 4;  // chunks of a stored tile-block: bf16 hi (bf16x3f) or hi + lo
-  static constexpr int SST = HALF ? 1 : 2;  // 8-byte stores per output tile
+  static constexpr int SST = HALF ? 1 : 2;  // 8-byte stores per output tile: hi [+ lo]
+  // (r6, measured and removed: the two 16-row tiles of one old tile stored together, one 16-byte store per lane
+  // with the halves exchanged by v_permlane32_swap -- bit-identical, bf16x3f training forward 1.502 -> 1.573 ms,
+  // bf16x3 1.660 -> 1.769; profiles/r6/pair_store_ab.json)
+  static constexpr int PRO_ST = 6 * SST;  // the prologue's PE stores (3 K-blocks x 2 halves)
   using GT = GroupTable<2, DENSITY, P::CH>;
   static_assert(finish_schedule_violation<P, 2, DENSITY>() == 0,
                 "finish placement (NERF_FINISH_PARTS_* / NERF_FINISH_DELAY) reads a tile pair before its finish part "
@@ -1894,7 +1898,7 @@ struct FwdWave16 {
     group_body<P, 2, DENSITY, gi>(*this, lds_ptr(sl + (uint32_t)(lane * 16)));
     constexpr int N = dma_spread<P>() > 0
         ? handoff_vmcnt_spread<P, 2, DENSITY>(gi, [](int u) constexpr { return unit_stores(u); })
-        : handoff_vmcnt<P, 2, DENSITY>(gi, [](int i) constexpr { return group_stores(i); }, STORE ? 6 * SST : 0);
+        : handoff_vmcnt<P, 2, DENSITY>(gi, [](int i) constexpr { return group_stores(i); }, STORE ? PRO_ST : 0);
     if constexpr (gi + 1 < NG) wait_barrier<N>();
   }
 
@@ -1922,7 +1926,7 @@ struct FwdWave16 {
     }
     {  // group 0 landed: younger = the DMAs of groups 1 .. PF - 1 and the PE stores (3 K-blocks x 2 halves)
       constexpr int N0 = [] {
-        int n = STORE ? 6 * SST : 0;
+        int n = STORE ? PRO_ST : 0;
         for (int j = 1; j < PF && j < GT::t.n; ++j) n += group_dma<P, 2, DENSITY>(j);
         return n;
       }();
@@ -3316,3 +3320,33 @@ int nerf_mlp_bwd(const void* packed_bwd, int dtype, const float* d_raw, int64_t 
 }  // extern "C"
 #endif  // !NERF_MLP_PREC
 #endif  // NERF_MLP_DEVICE_ONLY
+
+// ------------------------------------------------------------------------------------
+// Knob policy (round 6).  Schedule knobs -- NERF_FINISH_PARTS_*, NERF_FINISH_DELAY, NERF_PREFETCH_*,
+// NERF_DMA_SPREAD_*, NERF_GROUP_ACROSS -- may take any value: every placement they produce is proven at compile
+// time (FinishSchedule's static_assert in FwdWave / FwdWave16 / DxWave; the hand-off vmcnt counts are computed
+// from the same tables and tools/asm_check.py checks them on the emitted code).  NERF_BF3_WIDE selects
+// between two verified bf16x3 forwards.  NERF_DIAG_* are diagnostic builds only (results meaningless).  Every other tuning
+// knob is pinned to the value the tests verified: building another value fails here.
+// ------------------------------------------------------------------------------------
+#define NERF_PINNED(K, V) static_assert((K) == (V), #K ": only the verified value " #V " is allowed (mlp.hip knob policy)");
+NERF_PINNED(NERF_PACKED_MASK, 1)
+NERF_PINNED(NERF_DMA_LEAN, 1)
+NERF_PINNED(NERF_KEEP_PE_BF3, 1)
+NERF_PINNED(NERF_DW_NBUF_BF16, 4)
+NERF_PINNED(NERF_DW_SWZ_F32, 1)
+NERF_PINNED(NERF_DW_F32_PIPE, 1)
+NERF_PINNED(NERF_DW_FETCH_STEP, 1)
+NERF_PINNED(NERF_DW_FETCH_SPLIT, 4)
+NERF_PINNED(NERF_DW_DMA_NT, 1)
+#if defined(NERF_DW_BALANCE_MFMA)
+NERF_PINNED(NERF_DW_BALANCE_MFMA, 1)
+NERF_PINNED(NERF_DW_LAT_CYCLES, 4000)
+NERF_PINNED(NERF_DW_ITEMS_PER_CU, 2)
+NERF_PINNED(NERF_DW_COST_TABLE, 1)
+NERF_PINNED(NERF_DW_COST_TABLE_BF, 1)
+#endif
+#if defined(NERF_BF3_WIDE)
+static_assert(NERF_BF3_WIDE == 0 || NERF_BF3_WIDE == 1, "NERF_BF3_WIDE: 0 (32x32 bf16x3 forward) or 1 (wide)");
+#endif
+#undef NERF_PINNED
