@@ -73,3 +73,15 @@ def test_unsound_placement_fails_to_compile():
         good = subprocess.run([HIPCC, "--offload-arch=gfx950", "-std=c++17", f"-I{ROOT}/include", "--cuda-device-only",
                                "-fsyntax-only", "-DNERF_FINISH_PARTS_BF16=2", src], capture_output=True, text=True)
         assert good.returncode == 0, good.stderr[-2000:]
+
+
+def test_pinned_knobs_refuse_unverified_values():
+    """mlp.hip's knob policy: a tuning knob outside the schedule knobs builds only at its verified value."""
+    with tempfile.TemporaryDirectory() as tmp:
+        src = os.path.join(tmp, "k.hip")
+        with open(src, "w") as f:
+            f.write(f'#define NERF_MLP_DEVICE_ONLY\n#include "{MLP}"\n')
+        for knob in ("-DNERF_DW_NBUF_BF16=2", "-DNERF_PACKED_MASK=0", "-DNERF_DMA_LEAN=0", "-DNERF_KEEP_PE_BF3=0"):
+            bad = subprocess.run([HIPCC, "--offload-arch=gfx950", "-std=c++17", f"-I{ROOT}/include",
+                                  "--cuda-device-only", "-fsyntax-only", knob, src], capture_output=True, text=True)
+            assert bad.returncode != 0 and "knob policy" in bad.stderr, (knob, bad.stderr[-1500:])
