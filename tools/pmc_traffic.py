@@ -26,6 +26,8 @@ LABELS = {
     "fwd_kernel<nerf::mlp::PBF3, false, false,": "mlp_fwd",
     "dx_kernel<nerf::mlp::PBF3>": "mlp_bwd_dx",
     "dw_kernel<nerf::mlp::PBF3>": "mlp_bwd_dw",
+    "fwd_kernel<nerf::mlp::PBF3W, true, false,": "mlp_fwd_train",  # (the wide bf16x3 forward, round 6)
+    "fwd_kernel<nerf::mlp::PBF3W, false, false,": "mlp_fwd",
     "raygen_kernel(": "raygen",
     "stratified_kernel(": "sample_stratified",
     "sample_pdf_kernel(": "sample_pdf",
