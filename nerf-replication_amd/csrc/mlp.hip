@@ -567,6 +567,13 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef NERF_DIAG_NO_STORE
 #define NERF_DIAG_NO_STORE 0
 #endif
+// (NERF_DIAG_NO_MASK / NERF_DIAG_NO_ACT: the wide forward without its mask bits / without its activation stores)
+#ifndef NERF_DIAG_NO_MASK
+#define NERF_DIAG_NO_MASK 0
+#endif
+#ifndef NERF_DIAG_NO_ACT
+#define NERF_DIAG_NO_ACT 0
+#endif
 // (NERF_DIAG_STAMPS: diagnostic only -- the forward overwrites two raw rows per workgroup with its CU id and
 // entry / prologue-done / end timestamps, tools/wg_stamps.py)
 #ifndef NERF_DIAG_STAMPS
@@ -1641,7 +1648,7 @@ struct FwdWave {
 __device__ __forceinline__ void store8(char* p, uint32_t lo, uint32_t hi) {
   if constexpr (NERF_DIAG_NO_STORE) return;
   typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
-  __builtin_nontemporal_store((u32x2v){lo, hi}, (u32x2v*)p);
+  __builtin_nontemporal_store((u32x2v){lo, hi}, (u32x2v*)p);  // (plain stores measured: 1.536 -> 1.561 ms, r6)
 }
 __device__ __forceinline__ uint32_t get_dword(const bf16x8& v, int k) {
   const uint4 u = __builtin_bit_cast(uint4, v);
@@ -1705,7 +1712,7 @@ struct FwdWave16 {
   // (r6, measured and removed: the two 16-row tiles of one old tile stored together, one 16-byte store per lane
   // with the halves exchanged by v_permlane32_swap -- bit-identical, bf16x3f training forward 1.502 -> 1.573 ms,
   // bf16x3 1.660 -> 1.769; profiles/r6/pair_store_ab.json)
-  static constexpr int PRO_ST = 6 * SST;  // the prologue's PE stores (3 K-blocks x 2 halves)
+  static constexpr int PRO_ST = NERF_DIAG_NO_ACT ? 0 : 6 * SST;  // the prologue's PE stores (3 K-blocks x 2 halves)
   using GT = GroupTable<2, DENSITY, P::CH>;
   static_assert(finish_schedule_violation<P, 2, DENSITY>() == 0,
                 "finish placement (NERF_FINISH_PARTS_* / NERF_FINISH_DELAY) reads a tile pair before its finish part "
@@ -1771,9 +1778,10 @@ struct FwdWave16 {
   static __host__ __device__ constexpr int unit_stores(int u) {
     if (!STORE) return 0;
     const int L = fwd16_unit_layer(u), mt = u - fwd16_unit_first(L);
-    if (L == LFA) return mt < 16 ? SST : 0;
+    constexpr int ST = NERF_DIAG_NO_ACT ? 0 : SST, MS = NERF_DIAG_NO_MASK ? 0 : 1;
+    if (L == LFA) return mt < 16 ? ST : 0;
     if (L == LRGB) return 0;
-    return SST + (mt == fwd16_out_tiles(L) - 1 ? 1 : 0);  // + the layer's mask store
+    return ST + (mt == fwd16_out_tiles(L) - 1 ? MS : 0);  // + the layer's mask store
   }
   static __host__ __device__ constexpr int group_stores(int gi) {
     int n = 0;
@@ -1784,6 +1792,7 @@ struct FwdWave16 {
   // the training stores of one 32-feature tile (a K-block, or the two 16-row tiles that fill it): old
   // tile tau, 8 bytes of chunk c (hi) [and c + 2 (lo)] at this lane's slot
   __device__ __forceinline__ void store_half(int tau, int c, uint32_t h0, uint32_t h1, uint32_t l0, uint32_t l1) {
+    if constexpr (NERF_DIAG_NO_ACT) return;
     char* base = (char*)a.act + (((wb32 * AT_TILES + tau) * SCH + c) << 10) + st_off;
     store8(base, h0, h1);
     if constexpr (!HALF) store8(base + 2048, l0, l1);
@@ -1848,13 +1857,13 @@ struct FwdWave16 {
         }
         const uint32_t hw = pack_bf16(y0, y1);
         const uint32_t lw = pack_bf16(y0 - __uint_as_float(hw << 16), y1 - __uint_as_float(hw & 0xffff0000u));
-        if constexpr (STORE && RELU) bits |= nonzero_bf16x2(hw, one16) << k;  // bits k / 16 + k (as PBF3)
+        if constexpr (STORE && RELU && !NERF_DIAG_NO_MASK) bits |= nonzero_bf16x2(hw, one16) << k;  // (as PBF3)
         set_dword8(out.hi, Q + k, hw);
         set_dword8(out.lo, Q + k, lw);
       });
       if constexpr (STORE) {
         constexpr int n = mt >> 1, d = mt >> 2;  // old 32-row tile, its mask dword
-        if constexpr (RELU) {
+        if constexpr (RELU && !NERF_DIAG_NO_MASK) {
           // value 2k + j of this lane = old register rho = 4 (2 (mt & 1) + (g >> 1)) + 2k + j of old tile n, old
           // lane half h = g & 1: mask bit 8 (n & 1) + (rho >> 1) + 16 (rho & 1) = [bit k / 16 + k] << (C + gsh)
           constexpr uint32_t C = 8 * (n & 1) + 4 * (mt & 1);
@@ -1866,7 +1875,7 @@ struct FwdWave16 {
           constexpr int tau = (L == LV ? AT_V : L == LFA ? AT_F : AT_H + 8 * L) + n;
           store_half(tau, mt & 1, get_dword(out.hi, Q), get_dword(out.hi, Q + 1), get_dword(out.lo, Q),
                      get_dword(out.lo, Q + 1));
-          if constexpr (RELU && mt == fwd16_out_tiles(L) - 1) {
+          if constexpr (RELU && !NERF_DIAG_NO_MASK && mt == fwd16_out_tiles(L) - 1) {
             // old lane L gets its bits from lanes l and l + 32 (g = h, h + 2): OR in the partner's dwords; lanes l
             // and l + 32 then hold the same 16 bytes for the same old lane and both store them
             constexpr int ND = L == LV ? 2 : 4;

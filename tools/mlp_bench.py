@@ -280,6 +280,7 @@ def compare(args):
                 if r:
                     times[(name, k)].append(a.elapsed_time(e) / args.reps)
     out = {"M": M, "rounds": args.rounds}
+    out["packed_fwd_addr_mod_2MiB"] = {name: bufs[name]["pf"].data_ptr() % (2 << 20) for name, _ in libs}
     # the builds must compute the same thing: forward raw, the stored activations and the dX
     # stores, bit for bit (buffers zeroed first: padding a kernel never writes stays equal)
     n0 = libs[0][0]
