@@ -164,3 +164,53 @@ def test_config4_full_frame_march(g4, frame, renderer, dtype):
     print(f"march {dtype}: queried {out['n_queried']} (reference {ref_q}), evaluated {out['n_evaluated']}")
     allow = 16 if dtype != "bf16" else int(BF16_MARGIN * BF16_MEASURED["march"]["queried_offset"])
     assert abs(out["n_queried"] - ref_q) <= allow, (dtype, out["n_queried"] - ref_q)
+
+
+@pytest.mark.parametrize("dtype", ["bf16x3", "bf16x3f"])
+def test_selective_coarse_pass_scatter(g4, renderer, dtype):
+    """The opt-in selective coarse pass (round 6, volume_renderer.py) on the fixture's 4,096 sampled rays: every
+    ray flagged (abs_tol 2 > any CDF distance) renders exactly the default fp32-coarse render; with every
+    tolerance 0 the rays nerf_composite_pdf_fragile flags render exactly as the fp32-coarse render and all other
+    rays exactly as the render with the coarse net in the tier's own arithmetic -- the re-evaluation and its
+    scatter change the flagged rays and nothing else, bit for bit."""
+    from nerf_amd import ops
+    from src.config import cfg
+    net, r = renderer
+    net.mlp_dtype = dtype
+    dev = next(net.parameters()).device
+    rays = torch.from_numpy(g4["rays"]).to(dev)
+    near, far = torch.tensor([2.0], device=dev), torch.tensor([6.0], device=dev)
+    keys = ("fragile_rel_tol", "fragile_abs_tol", "fragile_den_tol", "fragile_z_tol")
+    saved = {k: cfg.task_arg.get(k) for k in ("coarse_inference_dtype",) + keys}
+
+    def render(mode, tols=(0.0, 0.0, 0.0, 0.0)):
+        cfg.task_arg.coarse_inference_dtype = mode
+        for k, v in zip(keys, tols):
+            cfg.task_arg[k] = v
+        r.fragile_rays = 0
+        with torch.no_grad():
+            return r.render({"rays": rays, "near": near, "far": far}), r.fragile_rays
+
+    try:
+        fp32, _ = render("fp32")
+        tier, _ = render(dtype)
+        allf, n_all = render("selective", (0.0, 2.0, 0.0, 0.0))
+        zero, n_zero = render("selective")
+        with torch.no_grad():  # the flags of the all-zero tolerances, as the renderer computes them
+            z, pts, vd = ops.sample_stratified(rays, near, far, int(cfg.task_arg.N_samples), False)
+            raw = net(pts, vd, "coarse", dtype=dtype)
+            flag = ops.composite_sample_pdf_fragile(raw, z, rays, bool(cfg.task_arg.white_bkgd),
+                                                    int(cfg.task_arg.N_importance), 0.0, 0.0)[4].bool()
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                cfg.task_arg.pop(k, None)
+            else:
+                cfg.task_arg[k] = v
+    assert n_all == rays.shape[0] and n_zero == int(flag.sum()), (n_all, n_zero, int(flag.sum()))
+    assert any(not torch.equal(fp32[k], tier[k]) for k in RENDER_KEYS)  # (the two coarse passes differ)
+    print(f"\nselective {dtype}: {n_zero} of {rays.shape[0]} rays flagged at zero tolerances")
+    for k in RENDER_KEYS:
+        assert torch.equal(allf[k], fp32[k]), k
+        assert torch.equal(zero[k][flag], fp32[k][flag]), k
+        assert torch.equal(zero[k][~flag], tier[k][~flag]), k
