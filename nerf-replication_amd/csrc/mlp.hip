@@ -47,7 +47,7 @@ __device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
 // ------------------------------------------------------------------------------------
 // precision policies
 // ------------------------------------------------------------------------------------
-enum PKind { K_F32 = 0, K_BF16 = 1, K_BF16X3 = 2, K_BF16X6 = 3, K_BF16X3W = 4 };
+enum PKind { K_F32 = 0, K_BF16 = 1, K_BF16X3 = 2, K_BF16X6 = 3, K_BF16X3W = 4, K_F32W = 5 };
 
 struct PF32 {
   static constexpr int KIND = K_F32;
@@ -325,7 +325,43 @@ struct PBF3W {
     const __bf16 h = (__bf16)x;
     return c == 0 ? h : (__bf16)(x - (float)h);
   }
+  // packed weight element e of chunk c, lane group g: feature k16_feat(g, e) of the K-block, split part c
+  static __host__ __device__ constexpr int feat16(int, int g, int e) { return k16_feat(g, e); }
+  static __host__ __device__ constexpr int part16(int c) { return c; }
 };
+
+// The wide fp32 TRAINING forward (round 6, PF32W): the PBF3W structure on v_mfma_f32_16x16x4_f32 -- one wave =
+// 16 samples, 8 waves per workgroup, two per SIMD (the 32x32x2 fp32 forward holds 32 samples' fp32 tiles in
+// ~450 registers: one wave per SIMD).  A K-block (32 features x 16 samples) is 8 MFMAs; MFMA j's B operand in
+// lane (s, g) is feature 16 (j >> 2) + 4 g + (j & 3) = k16_feat(g, j), so a 16x16 output tile mt (rows 4 g + e
+// in lane g) IS registers 4 (mt & 1) + e of the next layer's K-block mt >> 1.  Chunk c (1 KiB) of a K-block =
+// MFMAs 4c .. 4c + 3: lane l = r16 + 16 g reads W[r16][16 c + 4 g + 0..3], four contiguous fp32.  Same
+// arithmetic as PF32 (fp32 products, fp32 accumulation, libm PE), another summation order: the training forward
+// only -- renders keep PF32's order, which the full-frame fixtures are pinned against.
+struct PF32W {
+  static constexpr int KIND = K_F32W;
+  using Acc = f32x4;
+  static constexpr int SPW = 16;
+  static constexpr int CH = 2;
+  static constexpr int E = 4;
+  static constexpr int WAVES = 8;
+  static constexpr int ESIZE = 4;
+  static constexpr int SPL = 4;
+  static constexpr int PE = 1;  // PE_LIBM, as PF32
+  using Store = float;
+  struct Tile { float v[8]; };
+  static __device__ __forceinline__ f32x4 mma(uint4 a, const Tile& b, int c, f32x4 acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), b.v[4 * c + 0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), b.v[4 * c + 1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), b.v[4 * c + 2], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), b.v[4 * c + 3], acc, 0, 0, 0);
+  }
+  static __host__ __device__ constexpr int rho_of(int c, int e) { return 4 * c + e; }
+  static __device__ __forceinline__ Store cvt_c(float x, int) { return x; }
+  static __host__ __device__ constexpr int feat16(int c, int g, int e) { return 16 * c + 4 * g + e; }
+  static __host__ __device__ constexpr int part16(int) { return 0; }
+};
+template <class P> __host__ __device__ constexpr bool wide_kind() { return P::KIND == K_BF16X3W || P::KIND == K_F32W; }
 
 // ReLU-mask bit of accumulator register rho of a tile: the tile's 16 bits sit at positions
 // (rho >> 1) + 16 (rho & 1) of a dword (bf16 pair k = registers 2k, 2k+1 -> bits k, 16 + k),
@@ -408,9 +444,10 @@ __device__ __forceinline__ void pack_sources(int64_t i, const UnitOffsets& uo, W
   int u = 0;
   for (int k = 1; k < nunit; ++k) u += uo.off[k] <= chunk ? 1 : 0;
   const int within = chunk - uo.off[u];
-  if (DIR == 2) {
-    // 16-row unit (PBF3W): lane l = r16 + 16 g holds weight row r16 of the unit, the 8 features
-    // k16_feat(g, e) of K-block t; chunk c = 0 the hi, 1 the lo halves.  Bias chunk: lanes 0..3 hold
+  if constexpr (DIR == 2) {
+    // 16-row unit (PBF3W, PF32W): lane l = r16 + 16 g holds weight row r16 of the unit, the E features
+    // P::feat16(c, g, e) of K-block t, split part P::part16(c) (PBF3W: all 8 features of lane group g, chunk
+    // c = 0 the hi, 1 the lo halves; PF32W: the 4 features 16 c + 4 g + e).  Bias chunk: lanes 0..3 hold
     // rows 4 lane + e (the accumulator's rows of lane group g = lane), rest zero.
     const int L = fwd16_unit_layer(u), m = u - fwd16_unit_first(L);
     const int w = fwd16_out_weight(L, m);
@@ -425,10 +462,11 @@ __device__ __forceinline__ void pack_sources(int64_t i, const UnitOffsets& uo, W
     const int t = within / P::CH, c = within % P::CH, r16 = lane & 15, g = lane >> 4;
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
-      const int f = k16_feat(g, e);
+      const int f = P::feat16(c, g, e);
       const bool ok = r16 < fwd16_out_valid(L, m) && f < fwd_in_valid(L, t);
       weight(e, ok ? w : -1,
-             ok ? (int64_t)(fwd16_out_row0(L, m) + r16) * weight_K(w) + fwd_in_colbase(L, t) + f : (int64_t)0, c);
+             ok ? (int64_t)(fwd16_out_row0(L, m) + r16) * weight_K(w) + fwd_in_colbase(L, t) + f : (int64_t)0,
+             P::part16(c));
     }
     return;
   }
@@ -750,8 +788,11 @@ __host__ __device__ constexpr Step group_step(int g, int k) {
 #ifndef NERF_FINISH_DELAY
 #define NERF_FINISH_DELAY 3
 #endif
+#ifndef NERF_PREFETCH_F32W
+#define NERF_PREFETCH_F32W 2  // (a PF32W step is four 32-cycle MFMAs)
+#endif
 template <class P> __host__ __device__ constexpr int prefetch_depth() {
-  return P::KIND == K_F32 ? NERF_PREFETCH_F32 : NERF_PREFETCH_BF16;  // a bf16 / bf16x3 step is 1-2 short MFMAs
+  return P::KIND == K_F32 ? NERF_PREFETCH_F32 : P::KIND == K_F32W ? NERF_PREFETCH_F32W : NERF_PREFETCH_BF16;  // a bf16 / bf16x3 step is 1-2 short MFMAs
 }
 constexpr int FINISH_DELAY = NERF_FINISH_DELAY;
 
@@ -801,9 +842,13 @@ __host__ __device__ constexpr bool finished_in_group(int g, int u) {
 #ifndef NERF_FINISH_PARTS_BF3W
 #define NERF_FINISH_PARTS_BF3W 2  // (a 16x16 tile's 2 register pairs)
 #endif
+#ifndef NERF_FINISH_PARTS_F32W
+#define NERF_FINISH_PARTS_F32W 2
+#endif
 template <class P> __host__ __device__ constexpr int finish_parts() {
   return P::KIND == K_F32 ? NERF_FINISH_PARTS_F32 : P::KIND == K_BF16 ? NERF_FINISH_PARTS_BF16
-       : P::KIND == K_BF16X3W ? NERF_FINISH_PARTS_BF3W : NERF_FINISH_PARTS_BF3;
+       : P::KIND == K_BF16X3W ? NERF_FINISH_PARTS_BF3W : P::KIND == K_F32W ? NERF_FINISH_PARTS_F32W
+       : NERF_FINISH_PARTS_BF3;
 }
 // DMA spread.  0: the next group's LDS-DMA pieces (up to 18 per wave, ~7 instructions each)
 // are issued as one burst at the group's start; S > 0: piece i at step i (NS / S) / NF of the
@@ -820,9 +865,12 @@ template <class P> __host__ __device__ constexpr int finish_parts() {
 #ifndef NERF_DMA_SPREAD_BF3W
 #define NERF_DMA_SPREAD_BF3W 3
 #endif
+#ifndef NERF_DMA_SPREAD_F32W
+#define NERF_DMA_SPREAD_F32W 3
+#endif
 template <class P> __host__ __device__ constexpr int dma_spread() {
   return PF != 1 ? 0 : P::KIND == K_F32 ? NERF_DMA_SPREAD_F32 : P::KIND == K_BF16 ? NERF_DMA_SPREAD_BF16
-       : P::KIND == K_BF16X3W ? NERF_DMA_SPREAD_BF3W : NERF_DMA_SPREAD_BF3;
+       : P::KIND == K_BF16X3W ? NERF_DMA_SPREAD_BF3W : P::KIND == K_F32W ? NERF_DMA_SPREAD_F32W : NERF_DMA_SPREAD_BF3;
 }
 
 // step (in group g) at which part p of unit u's finish is issued, or -1 when u is not
@@ -941,7 +989,7 @@ template <class P> __host__ __device__ constexpr int chunk_pairs(int c) {
   return m;
 }
 // pairs of an output tile: 8 (32x32 accumulator, 16 registers), 2 (16x16, 4 registers)
-template <class P> __host__ __device__ constexpr int tile_pairs() { return P::KIND == K_BF16X3W ? 2 : 8; }
+template <class P> __host__ __device__ constexpr int tile_pairs() { return wide_kind<P>() ? 2 : 8; }
 template <class P> __host__ __device__ constexpr int part_pairs(int p) {
   constexpr int NP = finish_parts<P>(), TP = tile_pairs<P>();
   int m = 0;
@@ -1339,7 +1387,7 @@ __device__ __forceinline__ uint4* mask_slot(void* masks, int64_t wblock, int grp
 #define NERF_KEEP_PE_BF3 1
 #endif
 template <class P> __host__ __device__ constexpr bool keep_pe() {
-  return (P::KIND == K_BF16X3 || P::KIND == K_BF16X3W) && NERF_KEEP_PE_BF3;
+  return (P::KIND == K_BF16X3 || P::KIND == K_BF16X3W || P::KIND == K_F32W) && NERF_KEEP_PE_BF3;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1667,8 +1715,8 @@ __device__ __forceinline__ void set_dword8(bf16x8& v, int k, uint32_t d) {
 template <class T> __device__ __forceinline__ T sel4(int g, T a0, T a1, T a2, T a3) {
   return (g & 2) ? ((g & 1) ? a3 : a2) : ((g & 1) ? a1 : a0);  // (branch-free selects on the lane group)
 }
-template <int TILE, int NFREQ, int NVALID>
-__device__ __forceinline__ void pe_kblock(PBF3W::Tile& t, int g, float x0, float x1, float x2) {
+template <class P, int TILE, int NFREQ, int NVALID>
+__device__ __forceinline__ void pe_kblock(typename P::Tile& t, int g, float x0, float x1, float x2) {
   constexpr double INV2PI = 0.15915494309189533576888376337251;
   float v[8];
   sfor<8>([&](auto ee) {
@@ -1683,32 +1731,46 @@ __device__ __forceinline__ void pe_kblock(PBF3W::Tile& t, int g, float x0, float
     const float x = sel4(g, c0, c1, c2, c3);
     float trig = 0.f;
     if constexpr (F0.kind == 2 || F1.kind == 2 || F2.kind == 2 || F3.kind == 2) {
-      const double srev = sel4(g, INV2PI * (double)(1 << F0.k), INV2PI * (double)(1 << F1.k),
-                               INV2PI * (double)(1 << F2.k), INV2PI * (double)(1 << F3.k));
-      const double ph = sel4(g, F0.cos ? 0.25 : 0.0, F1.cos ? 0.25 : 0.0, F2.cos ? 0.25 : 0.0, F3.cos ? 0.25 : 0.0);
-      trig = pe_trig<PE_POLY>(x, srev, 0.f, ph, false);
+      if constexpr (P::PE == PE_LIBM) {  // (PF32W: sincosf of the exact fp32 x * 2^k, as PF32's pe_tile)
+        const float srad = sel4(g, (float)(1 << F0.k), (float)(1 << F1.k), (float)(1 << F2.k), (float)(1 << F3.k));
+        const bool is_cos = sel4(g, F0.cos != 0, F1.cos != 0, F2.cos != 0, F3.cos != 0);
+        trig = pe_trig<PE_LIBM>(x, 0.0, srad, 0.0, is_cos);
+      } else {
+        const double srev = sel4(g, INV2PI * (double)(1 << F0.k), INV2PI * (double)(1 << F1.k),
+                                 INV2PI * (double)(1 << F2.k), INV2PI * (double)(1 << F3.k));
+        const double ph = sel4(g, F0.cos ? 0.25 : 0.0, F1.cos ? 0.25 : 0.0, F2.cos ? 0.25 : 0.0, F3.cos ? 0.25 : 0.0);
+        trig = pe_trig<PE_POLY>(x, srev, 0.f, ph, false);
+      }
     }
     v[e] = sel4(g, F0.kind == 2 ? trig : F0.kind == 1 ? x : 0.f, F1.kind == 2 ? trig : F1.kind == 1 ? x : 0.f,
                 F2.kind == 2 ? trig : F2.kind == 1 ? x : 0.f, F3.kind == 2 ? trig : F3.kind == 1 ? x : 0.f);
   });
-  uint32_t hw[4], lw[4];
+  if constexpr (P::KIND == K_F32W) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    hw[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
-    lw[k] = pack_bf16(v[2 * k] - __uint_as_float(hw[k] << 16), v[2 * k + 1] - __uint_as_float(hw[k] & 0xffff0000u));
+    for (int e = 0; e < 8; ++e) t.v[e] = v[e];
+  } else {
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hw[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
+      lw[k] = pack_bf16(v[2 * k] - __uint_as_float(hw[k] << 16), v[2 * k + 1] - __uint_as_float(hw[k] & 0xffff0000u));
+    }
+    t.hi = __builtin_bit_cast(bf16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
+    t.lo = __builtin_bit_cast(bf16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
   }
-  t.hi = __builtin_bit_cast(bf16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
-  t.lo = __builtin_bit_cast(bf16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
 }
 
-template <bool STORE, bool DENSITY, bool PERSIST = false, bool HALF = false>
+template <class P, bool STORE, bool DENSITY, bool PERSIST = false, bool HALF = false>
 struct FwdWave16 {
-  using P = PBF3W;
-  using Tile = P::Tile;
+  using Tile = typename P::Tile;
   using Acc = f32x4;
+  static constexpr bool F32 = P::KIND == K_F32W;
+  static_assert(wide_kind<P>() && (!HALF || (!F32 && STORE)), "FwdWave16: PBF3W (HALF: bf16x3f stores) or PF32W");
+  static_assert(!F32 || (STORE && !PERSIST), "PF32W: the training forward only");
   static constexpr int CH = P::CH;
-  static constexpr int SCH = HALF ? 2 : 4;  // chunks of a stored tile-block: bf16 hi (bf16x3f) or hi + lo
-  static constexpr int SST = HALF ? 1 : 2;  // 8-byte stores per output tile: hi [+ lo]
+  static constexpr int SCH = HALF ? 2 : 4;  // chunks of a stored tile-block: bf16 hi (bf16x3f), hi + lo, or fp32
+  // stores per output tile: PBF3W one 8-byte store per half (hi [+ lo]); PF32W one 16-byte store
+  static constexpr int SST = F32 ? 1 : HALF ? 1 : 2;
   // (r6, measured and removed: the two 16-row tiles of one old tile stored together, one 16-byte store per lane
   // with the halves exchanged by v_permlane32_swap -- bit-identical, bf16x3f training forward 1.502 -> 1.573 ms,
   // bf16x3 1.660 -> 1.769; profiles/r6/pair_store_ab.json)
@@ -1723,7 +1785,8 @@ struct FwdWave16 {
   int lane, wave, s, g;
   int64_t m;        // this lane's sample
   int64_t wb32;     // the 32-sample block of the training stores
-  uint32_t st_off;  // byte offset of this lane's 8 bytes in a 1-KiB chunk of the stores
+  uint32_t st_off;  // byte offset of this lane's 8 bytes in a 1-KiB chunk of the stores (PF32W: its 16 bytes,
+                    // + 1 KiB (g >> 1): chunk 2 (mt & 1) + (g >> 1) of the fp32 tile-block)
   uint32_t lold;    // old-layout lane of the mask store: sample (16 (wave & 1) + s) + 32 (g & 1)
   uint32_t gsh;     // 2 (g >> 1): offset of this lane's mask bits among an old register pair group
   float px, py, pz, dx, dy, dz;
@@ -1746,7 +1809,7 @@ struct FwdWave16 {
     wb32 = blk * (P::WAVES / 2) + (wave >> 1);
     const uint32_t sb = 16u * (uint32_t)(wave & 1) + (uint32_t)s;
     lold = sb + 32u * (uint32_t)(g & 1);
-    st_off = 16u * lold + 8u * (uint32_t)(g >> 1);
+    st_off = 16u * lold + (F32 ? 1024u : 8u) * (uint32_t)(g >> 1);
     gsh = 2u * (uint32_t)(g >> 1);
     one16 = opaque_one16();
     dl = DmaLean{a.wpack, (uint32_t)(lane * 16 + wave * 1024),
@@ -1797,9 +1860,22 @@ struct FwdWave16 {
     store8(base, h0, h1);
     if constexpr (!HALF) store8(base + 2048, l0, l1);
   }
+  // PF32W: output-tile half hf of fp32 tile tau (values v[4 hf .. 4 hf + 3]) = old lane lold's 16 bytes of chunk
+  // 2 hf + (g >> 1) (old register rho = 4 (2 hf + (g >> 1)) + e holds feature 16 hf + 4 g + e, acc_row)
+  __device__ __forceinline__ void store_f32(int tau, int hf, const Tile& t) {
+    if constexpr (NERF_DIAG_NO_ACT) return;
+    char* base = (char*)a.act + (((wb32 * AT_TILES + tau) * SCH + 2 * hf) << 10) + st_off;
+    store16<0>((uint4*)base, make_uint4(__float_as_uint(t.v[4 * hf]), __float_as_uint(t.v[4 * hf + 1]),
+                                        __float_as_uint(t.v[4 * hf + 2]), __float_as_uint(t.v[4 * hf + 3])));
+  }
   __device__ __forceinline__ void store_kblock(int tau, const Tile& t) {
-    store_half(tau, 0, get_dword(t.hi, 0), get_dword(t.hi, 1), get_dword(t.lo, 0), get_dword(t.lo, 1));
-    store_half(tau, 1, get_dword(t.hi, 2), get_dword(t.hi, 3), get_dword(t.lo, 2), get_dword(t.lo, 3));
+    if constexpr (F32) {
+      store_f32(tau, 0, t);
+      store_f32(tau, 1, t);
+    } else {
+      store_half(tau, 0, get_dword(t.hi, 0), get_dword(t.hi, 1), get_dword(t.lo, 0), get_dword(t.lo, 1));
+      store_half(tau, 1, get_dword(t.hi, 2), get_dword(t.hi, 3), get_dword(t.lo, 2), get_dword(t.lo, 3));
+    }
   }
 
   // ---- group_body hooks
@@ -1822,14 +1898,14 @@ struct FwdWave16 {
       settle(px);
       settle(py);
       settle(pz);
-      pe_kblock<0, 10, 63>(X[0], g, px, py, pz);
-      pe_kblock<1, 10, 63>(X[1], g, px, py, pz);
+      pe_kblock<P, 0, 10, 63>(X[0], g, px, py, pz);
+      pe_kblock<P, 1, 10, 63>(X[1], g, px, py, pz);
     }
     if constexpr (L == LV && mt == 0) {
       settle(dx);
       settle(dy);
       settle(dz);
-      pe_kblock<0, 4, 27>(D, g, dx, dy, dz);
+      pe_kblock<P, 0, 4, 27>(D, g, dx, dy, dz);
     }
     acc[0] = __uint_as_float(bias.x);
     acc[1] = __uint_as_float(bias.y);
@@ -1855,11 +1931,19 @@ struct FwdWave16 {
           y0 = __int_as_float(max(__float_as_int(y0), 0));
           y1 = __int_as_float(max(__float_as_int(y1), 0));
         }
-        const uint32_t hw = pack_bf16(y0, y1);
-        const uint32_t lw = pack_bf16(y0 - __uint_as_float(hw << 16), y1 - __uint_as_float(hw & 0xffff0000u));
-        if constexpr (STORE && RELU && !NERF_DIAG_NO_MASK) bits |= nonzero_bf16x2(hw, one16) << k;  // (as PBF3)
-        set_dword8(out.hi, Q + k, hw);
-        set_dword8(out.lo, Q + k, lw);
+        if constexpr (F32) {
+          // bits k / 16 + k: the pair's values non-zero (after the ReLU: > 0), the bf16 path's bit layout
+          if constexpr (STORE && RELU && !NERF_DIAG_NO_MASK)
+            bits |= (min((uint32_t)__float_as_int(y0), 1u) | (min((uint32_t)__float_as_int(y1), 1u) << 16)) << k;
+          out.v[2 * Q + 2 * k] = y0;
+          out.v[2 * Q + 2 * k + 1] = y1;
+        } else {
+          const uint32_t hw = pack_bf16(y0, y1);
+          const uint32_t lw = pack_bf16(y0 - __uint_as_float(hw << 16), y1 - __uint_as_float(hw & 0xffff0000u));
+          if constexpr (STORE && RELU && !NERF_DIAG_NO_MASK) bits |= nonzero_bf16x2(hw, one16) << k;  // (as PBF3)
+          set_dword8(out.hi, Q + k, hw);
+          set_dword8(out.lo, Q + k, lw);
+        }
       });
       if constexpr (STORE) {
         constexpr int n = mt >> 1, d = mt >> 2;  // old 32-row tile, its mask dword
@@ -1873,8 +1957,9 @@ struct FwdWave16 {
         }
         if constexpr (LASTP) {
           constexpr int tau = (L == LV ? AT_V : L == LFA ? AT_F : AT_H + 8 * L) + n;
-          store_half(tau, mt & 1, get_dword(out.hi, Q), get_dword(out.hi, Q + 1), get_dword(out.lo, Q),
-                     get_dword(out.lo, Q + 1));
+          if constexpr (F32) store_f32(tau, mt & 1, out);
+          else store_half(tau, mt & 1, get_dword(out.hi, Q), get_dword(out.hi, Q + 1), get_dword(out.lo, Q),
+                          get_dword(out.lo, Q + 1));
           if constexpr (RELU && !NERF_DIAG_NO_MASK && mt == fwd16_out_tiles(L) - 1) {
             // old lane L gets its bits from lanes l and l + 32 (g = h, h + 2): OR in the partner's dwords; lanes l
             // and l + 32 then hold the same 16 bytes for the same old lane and both store them
@@ -1924,11 +2009,11 @@ struct FwdWave16 {
       dz = a.dirs[di * 3 + 2];
     }
     sfor<(PF < GT::t.n ? PF : GT::t.n)>([&](auto gg) { fetch<decltype(gg)::value>(); });
-    pe_kblock<0, 10, 63>(X[0], g, px, py, pz);
-    pe_kblock<1, 10, 63>(X[1], g, px, py, pz);
+    pe_kblock<P, 0, 10, 63>(X[0], g, px, py, pz);
+    pe_kblock<P, 1, 10, 63>(X[1], g, px, py, pz);
     if constexpr (STORE) {
       Tile Dt;
-      pe_kblock<0, 4, 27>(Dt, g, dx, dy, dz);
+      pe_kblock<P, 0, 4, 27>(Dt, g, dx, dy, dz);
       store_kblock(AT_X, X[0]);
       store_kblock(AT_X + 1, X[1]);
       store_kblock(AT_D, Dt);
@@ -1951,7 +2036,7 @@ struct FwdWave16 {
 };
 
 template <class P, bool STORE, bool DENSITY, bool PERSIST, bool HALF>
-using FwdWaveOf = std::conditional_t<P::KIND == K_BF16X3W, FwdWave16<STORE, DENSITY, PERSIST, HALF>,
+using FwdWaveOf = std::conditional_t<wide_kind<P>(), FwdWave16<P, STORE, DENSITY, PERSIST, HALF>,
                                      FwdWave<P, STORE, DENSITY, PERSIST, HALF>>;
 
 // PERSIST (inference only): the sample count is read on the device (a.M_dev, e.g. the grid
@@ -2885,7 +2970,7 @@ namespace mlp {
 // guard on that device.  (round 6)
 static_assert(NET_PARAMS < (1 << 24), "a plan entry holds a 24-bit parameter offset");
 // the packed-weight layout of a policy's forward: 32-row units (0), or the 16-row units of PBF3W (2)
-template <class P> static constexpr int fwd_layout() { return P::KIND == K_BF16X3W ? 2 : 0; }
+template <class P> static constexpr int fwd_layout() { return wide_kind<P>() ? 2 : 0; }
 template <class P, class F> static void with_layout(int dir, F&& f) {  // f(integral_constant<layout>)
   if (dir == 1) {
     if constexpr (fwd_layout<P>() != 2) f(std::integral_constant<int, 1>{});  // (PBF3W: forward only)
@@ -2956,6 +3041,20 @@ void mlp_fwd_train_impl(const FwdArgs& a, hipStream_t stream) {
 #define NERF_BF3_WIDE 1
 #endif
 using PBF3F = std::conditional_t<NERF_BF3_WIDE != 0, PBF3W, PBF3>;
+// The fp32 TRAINING forward: PF32's, or with -DNERF_F32_WIDE=1 the wide 16x16x4 kernel (PF32W, round 6; the
+// inference forwards -- renders, the march, the bake -- stay PF32 either way: another summation order moves the
+// few ill-conditioned CDF bins of the full-frame fixtures).  The fp32 forward pack then holds both
+// layouts, PF32's units first (nerf_mlp_packed_bytes), and the training forward reads the second.  Not the
+// default (profiles/r6/f32w_*.json): 4.9 % faster (4.863 -> 4.625 ms per 524,288 samples), deterministic, masks
+// equal to its activations' non-zeros, raw within 2.7e-7 of PF32's -- but its summation order flips the ReLU
+// branch of a few near-zero pre-activations that PF32's order and the reference's agree on, and the 4,096-ray
+// fine-net L0 bias gradient then sits 9.4e-4 (of the tensor's largest) from the reference's against the fp32
+// contract's 1e-4 (PF32: 5.5e-5; tests/test_gpu_trained.py::test_loss_gradients_fp32).
+#ifndef NERF_F32_WIDE
+#define NERF_F32_WIDE 0
+#endif
+using PF32T = std::conditional_t<NERF_F32_WIDE != 0, PF32W, PF32>;
+[[maybe_unused]] constexpr int64_t F32W_PACK_OFF = NERF_F32_WIDE ? total_chunks(PF32::CH, 0) * 1024 : 0;
 // bf16x3 forward, bf16 (hi-half) stores for the bf16 backward
 void mlp_fwd_train_half_impl(const FwdArgs& a, hipStream_t stream);
 #if defined(NERF_MLP_PREC) && NERF_MLP_PREC == 2 && (!defined(NERF_MLP_PART) || NERF_MLP_PART == 4)
@@ -3000,6 +3099,10 @@ void mlp_dw_impl(const DwArgs& w, dim3 grid, hipStream_t stream) {
   NERF_MLP_I_FWDT(EXT, P) NERF_MLP_I_FWDI(EXT, P) NERF_MLP_I_FWDD(EXT, P) NERF_MLP_I_FWDP(EXT, P)
 #if !defined(NERF_MLP_PREC)
 NERF_MLP_IMPLS(extern, PF32)
+#if NERF_F32_WIDE
+NERF_MLP_I_FWDT(extern, PF32W)
+NERF_MLP_I_PACK(extern, PF32W)
+#endif
 NERF_MLP_IMPLS(extern, PBF16)
 NERF_MLP_I_PACK(extern, PBF3)  // bf16x3: the W^T pack, dX, dW (+ the forward pack when not wide)
 NERF_MLP_I_DX(extern, PBF3)
@@ -3030,8 +3133,13 @@ NERF_MLP_I_PACK(, PBF6)
 #else
 #define NERF_PP_FWD NERF_PP
 #endif
+#if NERF_MLP_PREC == 0
+#define NERF_PP_FWDT PF32T  // (the fp32 training forward: PF32W unless NERF_F32_WIDE=0)
+#else
+#define NERF_PP_FWDT NERF_PP_FWD
+#endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 0
-NERF_MLP_I_FWDT(, NERF_PP_FWD)
+NERF_MLP_I_FWDT(, NERF_PP_FWDT)
 #endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 1
 NERF_MLP_I_FWDI(, NERF_PP_FWD)
@@ -3047,6 +3155,9 @@ NERF_MLP_I_DX(, NERF_PP)
 NERF_MLP_I_PACK(, NERF_PP)
 #if NERF_MLP_PREC == 2 && NERF_BF3_WIDE
 NERF_MLP_I_PACK(, PBF3W)
+#endif
+#if NERF_MLP_PREC == 0 && NERF_F32_WIDE
+NERF_MLP_I_PACK(, PF32W)
 #endif
 #endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 3
@@ -3076,6 +3187,8 @@ int64_t nerf_mlp_packed_bytes(int dtype, int dir) {
   if (!train_dtype(dtype) || (dir != 0 && dir != 1)) return -1;
   const int p = dir == 0 ? fwd_prec(dtype) : bwd_prec(dtype);
   if (p == 2 && dir == 0) return total_chunks(PBF3F::CH, fwd_layout<PBF3F>()) * 1024;  // (the wide bf16x3 forward)
+  if (p == 0 && dir == 0 && NERF_F32_WIDE)  // PF32's units, then PF32W's (the training forward)
+    return F32W_PACK_OFF + total_chunks(PF32W::CH, fwd_layout<PF32W>()) * 1024;
   return total_chunks(p == 1 ? PBF16::CH : PF32::CH, dir) * 1024;  // bf16x3: CH 4 as fp32
 }
 
@@ -3105,7 +3218,10 @@ int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void*
     if (!dst) continue;
     const int p = dir == 0 ? fwd_prec(dtype) : bwd_prec(dtype);
     if (p == 4) mlp_pack_impl<PBF6>(prm, dir, (char*)dst, stream);
-    else if (p == 0) mlp_pack_impl<PF32>(prm, dir, (char*)dst, stream);
+    else if (p == 0) {
+      mlp_pack_impl<PF32>(prm, dir, (char*)dst, stream);
+      if (dir == 0 && NERF_F32_WIDE) mlp_pack_impl<PF32T>(prm, dir, (char*)dst + F32W_PACK_OFF, stream);
+    }
     else if (p == 1) mlp_pack_impl<PBF16>(prm, dir, (char*)dst, stream);
     else if (dir == 0) mlp_pack_impl<PBF3F>(prm, dir, (char*)dst, stream);
     else mlp_pack_impl<PBF3>(prm, dir, (char*)dst, stream);
@@ -3131,7 +3247,10 @@ int nerf_mlp_fwd(const void* packed_fwd, int dtype, const float* pts, const floa
   FwdArgs a{(const char*)packed_fwd, pts, viewdirs, dir_index, samples_per_dir, M,
             nerf_mlp_padded_samples(M) / 32, raw, act, masks};
   if (store) {
-    if (dtype == 0) mlp_fwd_train_impl<PF32>(a, stream);
+    if (dtype == 0) {
+      a.wpack += F32W_PACK_OFF;  // (the PF32W units of the fp32 pack)
+      mlp_fwd_train_impl<PF32T>(a, stream);
+    }
     else if (dtype == 1) mlp_fwd_train_impl<PBF16>(a, stream);
     else if (dtype == 2) mlp_fwd_train_impl<PBF3F>(a, stream);
     else mlp_fwd_train_half_impl(a, stream);

@@ -26,7 +26,8 @@ pytestmark = pytest.mark.skipif(shutil.which(HIPCC) is None, reason="no hipcc")
 CASES = [("PF32", 0, "false"), ("PF32", 0, "true"), ("PF32", 1, "false"),
          ("PBF16", 0, "false"), ("PBF16", 0, "true"), ("PBF16", 1, "false"),
          ("PBF3", 0, "false"), ("PBF3", 0, "true"), ("PBF3", 1, "false"), ("PBF6", 0, "false"),
-         ("PBF3W", 2, "false"), ("PBF3W", 2, "true")]  # (the wide bf16x3 forward: 16-row units)
+         ("PBF3W", 2, "false"), ("PBF3W", 2, "true"),  # (the wide bf16x3 forward: 16-row units)
+         ("PF32W", 2, "false")]  # (the wide fp32 training forward)
 
 
 def _violations(tmp, defines):

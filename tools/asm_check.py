@@ -23,10 +23,12 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # every MLP kernel instantiation the library builds: per precision the training, inference, density-only
 # and persistent forwards, dX and dW; the bf16x3f training forward (bf16 stores) and the bf16x6 forward
-# (the bf16x3 forwards are the wide PBF3W kernels since round 6; PBF3 keeps the bf16x3 dX / dW)
+# (the bf16x3 forwards are the wide PBF3W kernels since round 6; PBF3 keeps the bf16x3 dX / dW; the fp32 training
+# forward is the wide PF32W one)
 KERNELS = [f"fwd_kernel<nerf::mlp::{p}, {a}>" for p in ("PF32", "PBF16", "PBF3W")
            for a in ("true, false, false", "false, false, false", "false, true, false", "false, false, true")] + \
-          ["fwd_kernel<nerf::mlp::PBF3W, true, false, false, true>", "fwd_kernel<nerf::mlp::PBF6, false, false, false>"] + \
+          ["fwd_kernel<nerf::mlp::PBF3W, true, false, false, true>", "fwd_kernel<nerf::mlp::PBF6, false, false, false>",
+           "fwd_kernel<nerf::mlp::PF32W, true, false, false>"] + \
           [f"{k}_kernel<nerf::mlp::{p}>" for k in ("dx", "dw") for p in ("PF32", "PBF16", "PBF3")]
 
 

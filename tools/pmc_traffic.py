@@ -28,6 +28,7 @@ LABELS = {
     "dw_kernel<nerf::mlp::PBF3>": "mlp_bwd_dw",
     "fwd_kernel<nerf::mlp::PBF3W, true, false,": "mlp_fwd_train",  # (the wide bf16x3 forward, round 6)
     "fwd_kernel<nerf::mlp::PBF3W, false, false,": "mlp_fwd",
+    "fwd_kernel<nerf::mlp::PF32W, true, false,": "mlp_fwd_train",  # (the wide fp32 training forward, round 6)
     "raygen_kernel(": "raygen",
     "stratified_kernel(": "sample_stratified",
     "sample_pdf_kernel(": "sample_pdf",

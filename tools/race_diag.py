@@ -8,7 +8,8 @@ dX `runs` times on the FIRST build's masks (the same input for every build).  Re
   * masks against the masks implied by the same run's stored activations (a ReLU bit is set iff the
     stored post-ReLU value is non-zero): mismatching dwords per mask group (layer);
   * which dZ tiles (mlp_tables.h DzTile) differ run to run and against the first build.
-Prints one JSON line.  (dtypes bf16, bf16x3, bf16x3f: the mask bits follow the bf16 / hi halves.)
+Prints one JSON line.  (dtypes bf16, bf16x3, bf16x3f: the mask bits follow the bf16 / hi halves; fp32: the fp32
+activations.)
 """
 import argparse
 import ctypes
@@ -29,10 +30,15 @@ from mlp_bench import load_handle  # noqa: E402
 AT_TILES, AT_H, AT_V, ZT_TILES, MASK_GROUPS = 79, 3, 75, 78, 9
 
 
-def expected_masks(act, nblk):
-    """[nblk, 9, 64, 4] int32 masks implied by bf16 act tile-blocks [nblk, 79, 2 chunks, 64 lanes, 8]."""
-    nch = act.numel() // (nblk * AT_TILES * 1024)  # 2 (bf16 / bf16x3f) or 4 (bf16x3: hi, lo)
-    a = act.view(torch.int16).view(nblk, AT_TILES, nch, 64, 8)[:, :, :2]
+def expected_masks(act, nblk, fp32=False):
+    """[nblk, 9, 64, 4] int32 masks implied by act tile-blocks: bf16 [nblk, 79, 2 chunks, 64 lanes, 8] (chunks 0, 1:
+    registers 0-7, 8-15; bf16x3 adds its lo chunks 2, 3), fp32 [nblk, 79, 4 chunks, 64 lanes, 4]."""
+    if fp32:
+        a = act.view(torch.float32).view(nblk, AT_TILES, 4, 64, 4).permute(0, 1, 3, 2, 4).reshape(nblk, AT_TILES, 64, 16)
+        a = a.reshape(nblk, AT_TILES, 64, 2, 8).permute(0, 1, 3, 2, 4)  # -> [b, tau, chunk-of-8, lane, 8] as bf16's
+    else:
+        nch = act.numel() // (nblk * AT_TILES * 1024)  # 2 (bf16 / bf16x3f) or 4 (bf16x3: hi, lo)
+        a = act.view(torch.int16).view(nblk, AT_TILES, nch, 64, 8)[:, :, :2]
     out = torch.zeros(nblk, MASK_GROUPS, 64, 4, dtype=torch.int64, device=act.device)
     rho = torch.arange(16, device=act.device)
     bitpos = (rho >> 1) + 16 * (rho & 1)
@@ -100,7 +106,7 @@ def main():
                    .ne(0).float().mean())}
         mism = []
         for raw, act, masks in fw:
-            exp = expected_masks(act, nblk)
+            exp = expected_masks(act, nblk, fp32=args.dtype == "fp32")
             got = masks.view(torch.int32).view(nblk, MASK_GROUPS, 64, 4).to(torch.int64) & 0xFFFFFFFF
             bad = (exp != got)
             mism.append([int(bad[:, g].sum()) for g in range(MASK_GROUPS)])
