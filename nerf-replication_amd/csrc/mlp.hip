@@ -403,17 +403,23 @@ constexpr int M_ALIGN = 256;  // activation stores are padded to this many sampl
 //   backward unit u: bwd_unit_tiles(u) * CH weight chunks
 // ------------------------------------------------------------------------------------
 // DIR 0: forward units, 1: dX-chain units, 2: 16-row forward units (PBF3W)
-__host__ __device__ constexpr int num_units(int dir) { return dir == 0 ? NUNIT_FWD : dir == 1 ? NUNIT_BWD : NUNIT_FWD16; }
+// DIR 3: 16-row dX units (PF32W / PBF3W)
+__host__ __device__ constexpr int num_units(int dir) {
+  return dir == 0 ? NUNIT_FWD : dir == 1 ? NUNIT_BWD : dir == 2 ? NUNIT_FWD16 : NUNIT_BWD16;
+}
 __host__ __device__ constexpr int fwd_unit_chunks(int u, int ch) { return fwd_unit_tiles(u) * ch + 1; }
 __host__ __device__ constexpr int fwd16_unit_chunks(int u, int ch) { return fwd16_unit_tiles(u) * ch + 1; }
 __host__ __device__ constexpr int fwd16_unit_chunk_off(int u, int ch) { return fwd16_unit_tile_off(u) * ch + u; }
 __host__ __device__ constexpr int fwd_unit_chunk_off(int u, int ch) { return fwd_unit_tile_off(u) * ch + u; }
 __host__ __device__ constexpr int bwd_unit_chunks(int u, int ch) { return bwd_unit_tiles(u) * ch; }
 __host__ __device__ constexpr int bwd_unit_chunk_off(int u, int ch) { return bwd_unit_tile_off(u) * ch; }
+__host__ __device__ constexpr int bwd16_unit_chunks(int u, int ch) { return bwd16_unit_tiles(u) * ch; }
+__host__ __device__ constexpr int bwd16_unit_chunk_off(int u, int ch) { return bwd16_unit_tile_off(u) * ch; }
 __host__ __device__ constexpr int64_t total_chunks(int ch, int dir) {
   return dir == 0 ? (int64_t)FWD_TILES * ch + NUNIT_FWD
        : dir == 1 ? (int64_t)BWD_TILES * ch
-       : (int64_t)FWD16_TILES * ch + NUNIT_FWD16;
+       : dir == 2 ? (int64_t)FWD16_TILES * ch + NUNIT_FWD16
+       : (int64_t)BWD16_TILES * ch;
 }
 
 struct ParamPtrs { const float* p[NPARAM]; };
@@ -427,7 +433,8 @@ constexpr UnitOffsets unit_offsets() {
   UnitOffsets t{};
   const int nu = num_units(DIR);
   for (int u = 0; u <= nu; ++u)
-    t.off[u] = DIR == 0 ? fwd_unit_chunk_off(u, CH) : DIR == 1 ? bwd_unit_chunk_off(u, CH) : fwd16_unit_chunk_off(u, CH);
+    t.off[u] = DIR == 0 ? fwd_unit_chunk_off(u, CH) : DIR == 1 ? bwd_unit_chunk_off(u, CH)
+             : DIR == 2 ? fwd16_unit_chunk_off(u, CH) : bwd16_unit_chunk_off(u, CH);
   return t;
 }
 
@@ -467,6 +474,21 @@ __device__ __forceinline__ void pack_sources(int64_t i, const UnitOffsets& uo, W
       weight(e, ok ? w : -1,
              ok ? (int64_t)(fwd16_out_row0(L, m) + r16) * weight_K(w) + fwd_in_colbase(L, t) + f : (int64_t)0,
              P::part16(c));
+    }
+    return;
+  }
+  if constexpr (DIR == 3) {
+    // 16-row dX unit (PF32W / PBF3W): half m & 1 of W^T output tile m >> 1 of stage s.  Lane l = r16 + 16 g holds
+    // A[i][p] = W[p][i] for dX row i = the forward in-feature bwd_out_colbase + 16 (m & 1) + r16 and the E forward
+    // out-features p = row0 + P::feat16(c, g, e) of input K-block t (forward output tile t of the stage's layer)
+    const int s = bwd16_unit_stage(u), m = u - bwd16_unit_first(s), L = bwd_fwd_layer(s);
+    const int t = within / P::CH, c = within % P::CH, r16 = lane & 15, g = lane >> 4;
+    const int w = fwd_out_weight(L, t), i = bwd_out_colbase(s, m >> 1) + 16 * (m & 1) + r16;
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int f = P::feat16(c, g, e);
+      const bool ok = f < fwd_out_valid(L, t);
+      weight(e, ok ? w : -1, ok ? (int64_t)(fwd_out_row0(L, t) + f) * weight_K(w) + i : (int64_t)0, P::part16(c));
     }
     return;
   }
@@ -666,18 +688,20 @@ struct Group { int u0, n, c0, nch; };  // first unit, units, first chunk, chunks
 // DIR 1: dX-chain units; DIR 2: 16-row forward units (PBF3W)
 template <int DIR, bool DENSITY>
 __host__ __device__ constexpr bool unit_used(int u) {
-  return DIR == 1 || !DENSITY ||
+  return DIR == 1 || DIR == 3 || !DENSITY ||
          (DIR == 0 ? (u < fwd_unit_first(LFA) || u == fwd_unit_first(LFA) + 8)
                    : (u < fwd16_unit_first(LFA) || u == fwd16_unit_first(LFA) + 16));
 }
 template <int DIR> __host__ __device__ constexpr int unit_seg(int u) {
-  return DIR == 0 ? fwd_unit_layer(u) : DIR == 1 ? bwd_unit_stage(u) : fwd16_unit_layer(u);
+  return DIR == 0 ? fwd_unit_layer(u) : DIR == 1 ? bwd_unit_stage(u) : DIR == 2 ? fwd16_unit_layer(u) : bwd16_unit_stage(u);
 }
 template <int DIR> __host__ __device__ constexpr int unit_chunks(int u, int ch) {
-  return DIR == 0 ? fwd_unit_chunks(u, ch) : DIR == 1 ? bwd_unit_chunks(u, ch) : fwd16_unit_chunks(u, ch);
+  return DIR == 0 ? fwd_unit_chunks(u, ch) : DIR == 1 ? bwd_unit_chunks(u, ch)
+       : DIR == 2 ? fwd16_unit_chunks(u, ch) : bwd16_unit_chunks(u, ch);
 }
 template <int DIR> __host__ __device__ constexpr int unit_chunk_off(int u, int ch) {
-  return DIR == 0 ? fwd_unit_chunk_off(u, ch) : DIR == 1 ? bwd_unit_chunk_off(u, ch) : fwd16_unit_chunk_off(u, ch);
+  return DIR == 0 ? fwd_unit_chunk_off(u, ch) : DIR == 1 ? bwd_unit_chunk_off(u, ch)
+       : DIR == 2 ? fwd16_unit_chunk_off(u, ch) : bwd16_unit_chunk_off(u, ch);
 }
 
 // greedy grouping: consecutive used units of one segment while the slot has room
@@ -754,7 +778,7 @@ __host__ __device__ constexpr int handoff_vmcnt(int g, StoresFn stores, int prol
 
 struct Step { int j, u, t, c, off, kin, len; bool first, last; };
 template <int DIR> __host__ __device__ constexpr int unit_tiles(int u) {
-  return DIR == 0 ? fwd_unit_tiles(u) : DIR == 1 ? bwd_unit_tiles(u) : fwd16_unit_tiles(u);
+  return DIR == 0 ? fwd_unit_tiles(u) : DIR == 1 ? bwd_unit_tiles(u) : DIR == 2 ? fwd16_unit_tiles(u) : bwd16_unit_tiles(u);
 }
 template <int DIR, bool DENSITY, int CH>
 __host__ __device__ constexpr int group_steps(int g) {
@@ -967,17 +991,20 @@ __host__ __device__ constexpr int bwd_out_slot(int s, int j) {
 template <int DIR> __host__ __device__ constexpr int unit_in_slot(int u, int t) {
   return DIR == 0 ? fwd_in_slot(fwd_unit_layer(u), t)
        : DIR == 1 ? bwd_in_slot(bwd_unit_stage(u), t)
-       : fwd_in_slot(fwd16_unit_layer(u), t);
+       : DIR == 2 ? fwd_in_slot(fwd16_unit_layer(u), t)
+       : bwd_in_slot(bwd16_unit_stage(u), t);
 }
 // 16-row unit (DIR 2): output tile m fills half m & 1 (elements 4 (m & 1) .. + 3) of K-block slot m >> 1
 template <int DIR> __host__ __device__ constexpr int unit_out_slot(int u) {
   return DIR == 0 ? fwd_out_slot(fwd_unit_layer(u), u - fwd_unit_first(fwd_unit_layer(u)))
        : DIR == 1 ? bwd_out_slot(bwd_unit_stage(u), u - bwd_unit_first(bwd_unit_stage(u)))
-       : fwd_out_slot(fwd16_unit_layer(u), (u - fwd16_unit_first(fwd16_unit_layer(u))) >> 1);
+       : DIR == 2 ? fwd_out_slot(fwd16_unit_layer(u), (u - fwd16_unit_first(fwd16_unit_layer(u))) >> 1)
+       : bwd_out_slot(bwd16_unit_stage(u), (u - bwd16_unit_first(bwd16_unit_stage(u))) >> 1);
 }
 // the register pairs of its slot a unit's finish writes (a 32x32 tile: all 8; a 16-row unit: 2 of a K-block's 4)
 template <int DIR> __host__ __device__ constexpr int unit_out_pairs(int u) {
-  return DIR != 2 ? 0xFF : (((u - fwd16_unit_first(fwd16_unit_layer(u))) & 1) ? 0xC : 0x3);
+  return DIR == 2 ? (((u - fwd16_unit_first(fwd16_unit_layer(u))) & 1) ? 0xC : 0x3)
+       : DIR == 3 ? (((u - bwd16_unit_first(bwd16_unit_stage(u))) & 1) ? 0xC : 0x3) : 0xFF;
 }
 // register pairs (bit k = registers 2k, 2k + 1) of a tile that MFMA chunk c reads / finish part p writes
 template <class P> __host__ __device__ constexpr int chunk_pairs(int c) {
@@ -998,7 +1025,7 @@ template <class P> __host__ __device__ constexpr int part_pairs(int p) {
 }
 // the pairs of its slot part p of unit u writes
 template <class P, int DIR> __host__ __device__ constexpr int part_write_pairs(int u, int p) {
-  return DIR != 2 ? part_pairs<P>(p) : part_pairs<P>(p) << (unit_out_pairs<DIR>(u) == 0xC ? 2 : 0);
+  return DIR < 2 ? part_pairs<P>(p) : part_pairs<P>(p) << (unit_out_pairs<DIR>(u) == 0xC ? 2 : 0);
 }
 // Positions in the straight-line schedule: 4 * (global step) + phase, the phases of one step in
 // group_body's order: 0 DMA pieces, 1 pend / init + MFMA, 2 the previous unit's finish parts, 3 the
@@ -1041,7 +1068,10 @@ struct FinishSchedule {
   __host__ __device__ constexpr int check() const {
     const auto& T = GroupTable<DIR, DENSITY, P::CH>::t;
     int out[NUNIT_MAX] = {}, opairs[NUNIT_MAX] = {}, pw[NUNIT_MAX][8] = {}, next_w[NUNIT_MAX][8] = {};
+    int ntiles[NUNIT_MAX] = {}, in_slot[NUNIT_MAX][10] = {};  // (precomputed: the unit walks are loops)
     for (int u = 0; u < NU; ++u) {
+      ntiles[u] = unit_tiles<DIR>(u);
+      for (int t = 0; t < ntiles[u]; ++t) in_slot[u][t] = unit_in_slot<DIR>(u, t);
       out[u] = unit_used<DIR, DENSITY>(u) ? unit_out_slot<DIR>(u) : (int)TS_NONE;
       opairs[u] = finish_slot(out[u]) ? unit_out_pairs<DIR>(u) : 0;
       for (int p = 0; p < NP; ++p) pw[u][p] = part_write_pairs<P, DIR>(u, p);
@@ -1074,17 +1104,17 @@ struct FinishSchedule {
     int writer[TS_X][8] = {};
     for (int sl = 0; sl < TS_X; ++sl)
       for (int q = 0; q < 8; ++q) writer[sl][q] = -1;
-    int base = 0;
+    int base = 0, done = 0;  // (writer holds the units < done, in unit order)
     for (int g = 0; g < T.n; ++g) {
       const Group G = T.g[g];
       for (int j = 0; j < G.n; ++j) {
         const int u = G.u0 + j;
-        for (int v = (j == 0 ? 0 : u - 1); v < u; ++v)
+        for (; done < u; ++done)
           for (int q = 0; q < 8; ++q)
-            if ((opairs[v] >> q) & 1) writer[out[v]][q] = v;
-        const int nt = unit_tiles<DIR>(u);
+            if ((opairs[done] >> q) & 1) writer[out[done]][q] = done;
+        const int nt = ntiles[u];
         for (int t = 0; t < nt; ++t) {
-          const int slot = unit_in_slot<DIR>(u, t);
+          const int slot = in_slot[u][t];
           if (!finish_slot(slot)) {
             base += P::CH;
             continue;
@@ -2072,6 +2102,14 @@ __global__ void __launch_bounds__(P::WAVES * 64) fwd_kernel(FwdArgs a) {
 // layer's output gradient (pre-activation dZ) fragment-native for the dW GEMMs.
 // Stages (mlp_tables.h BStage): bRGB -> dZv, bV -> dfeature, bFA -> dZ7, b7..b1 -> dZ6..dZ0.
 // ------------------------------------------------------------------------------------
+// (dz tile, mask group or -1) of output tile j of dX stage s
+__host__ __device__ constexpr int bwd_dz_tile(int s, int j) {
+  return s == B_RGB ? ZT_V + j : s == B_V ? ZT_F + j : s == B_FA ? ZT_H + 56 + j : ZT_H + 8 * (bwd_fwd_layer(s) - 1) + j;
+}
+__host__ __device__ constexpr int bwd_mask_group(int s) {
+  return s == B_RGB ? 8 : s == B_V ? -1 : s == B_FA ? 7 : bwd_fwd_layer(s) - 1;
+}
+
 struct DxArgs {
   const char* wpack_t;  // W^T chunks
   const float* d_raw;   // [M,4]
@@ -2138,13 +2176,8 @@ struct DxWave {
     }
   }
   template <int s, int t> __device__ __forceinline__ const Tile& in_tile_S() { return slot<bwd_in_slot(s, t)>(); }
-  // (dz tile, mask group or -1) of output tile j of stage s
-  static __host__ __device__ constexpr int dz_tile(int s, int j) {
-    return s == B_RGB ? ZT_V + j : s == B_V ? ZT_F + j : s == B_FA ? ZT_H + 56 + j : ZT_H + 8 * (bwd_fwd_layer(s) - 1) + j;
-  }
-  static __host__ __device__ constexpr int mask_group(int s) {
-    return s == B_RGB ? 8 : s == B_V ? -1 : s == B_FA ? 7 : bwd_fwd_layer(s) - 1;
-  }
+  static __host__ __device__ constexpr int dz_tile(int s, int j) { return bwd_dz_tile(s, j); }
+  static __host__ __device__ constexpr int mask_group(int s) { return bwd_mask_group(s); }
   static __host__ __device__ constexpr int group_stores(int g) {
     int s = 0;
     for (int u = 0; u < NUNIT_BWD; ++u)
@@ -2240,10 +2273,203 @@ struct DxWave {
   }
 };
 
+// ------------------------------------------------------------------------------------
+// The wide dX (round 6, PF32W / PBF3W): DxWave's W^T chain over 16-row units (DIR 3) on the 16x16 MFMAs, 16
+// samples per wave, 8 waves per workgroup, two per SIMD.  The same register trick as FwdWave16 (a 16-row output
+// tile IS half of the next stage's K-block), the forward's ReLU masks read from the old-layout lane of this
+// lane's sample and half (lold), and the dZ stores in the old tile-block layout (the dW is unchanged): lane
+// (s, g)'s four values of output tile m are old lane lold's registers 4 (2 (m & 1) + (g >> 1)) + e.
+// ------------------------------------------------------------------------------------
+template <class P>
+struct DxWave16 {
+  using Tile = typename P::Tile;
+  using Acc = f32x4;
+  static constexpr bool F32 = P::KIND == K_F32W;
+  static_assert(wide_kind<P>(), "DxWave16: PF32W or PBF3W");
+  static constexpr int CH = P::CH;
+  static constexpr int SCH = 4;             // chunks of a stored dZ tile-block (fp32, or bf16x3 hi + lo)
+  static constexpr int SST = F32 ? 1 : 2;   // stores per output tile: one 16-byte (fp32) or hi + lo 8-byte
+  using GT = GroupTable<3, false, P::CH>;
+  static_assert(finish_schedule_violation<P, 3, false>() == 0,
+                "finish placement (NERF_FINISH_PARTS_* / NERF_FINISH_DELAY) reads a tile pair before its finish part "
+                "writes it, or reads a reassigned pend (FinishSchedule)");
+
+  const DxArgs& a;
+  uint32_t lds_base;
+  int lane, wave, s, g;
+  int64_t m, wb32;
+  uint32_t st_off, lold, gsh;
+  Tile G, DA, Ha[8], Hb[8];
+  uint4 mk[MASK_GROUPS];
+  Acc pend;
+  DmaLean dl;
+
+  __device__ __forceinline__ DxWave16(const DxArgs& args, const uint4* smem) : a(args) {
+    lds_base = (uint32_t)(uintptr_t)(lds_void*)smem;
+    lane = threadIdx.x & 63;
+    wave = threadIdx.x >> 6;
+    s = lane & 15;
+    g = lane >> 4;
+    m = ((int64_t)blockIdx.x * P::WAVES + wave) * 16 + s;
+    wb32 = (int64_t)blockIdx.x * (P::WAVES / 2) + (wave >> 1);
+    lold = 16u * (uint32_t)(wave & 1) + (uint32_t)s + 32u * (uint32_t)(g & 1);
+    st_off = 16u * lold + (F32 ? 1024u : 8u) * (uint32_t)(g >> 1);
+    gsh = 2u * (uint32_t)(g >> 1);
+    dl = DmaLean{a.wpack_t, (uint32_t)(lane * 16 + wave * 1024),
+                 (uint32_t)__builtin_amdgcn_readfirstlane(lds_base + (uint32_t)wave * 1024u),
+                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)wave)};
+  }
+
+  template <int gi> __device__ __forceinline__ void fetch() {
+    constexpr Group Gr = GT::t.g[gi];
+    fetch_group_lean<P, Gr.c0, Gr.nch, (gi % NSLOT) * SLOT_CAP * 1024>(dl);
+  }
+  template <int gi, int i> __device__ __forceinline__ void fetch_piece() {
+    constexpr Group Gr = GT::t.g[gi];
+    fetch_piece_lean<P, Gr.c0, Gr.nch, (gi % NSLOT) * SLOT_CAP * 1024, i>(dl);
+  }
+  static __host__ __device__ constexpr int unit_stores(int) { return SST; }
+  static __host__ __device__ constexpr int group_stores(int gi) {
+    int n = 0;
+    for (int u = 0; u < NUNIT_BWD16; ++u)
+      if (finished_in_group<3, false, P::CH, cross_finish<P, 3>()>(gi, u)) n += SST;
+    return n;
+  }
+  template <int S> __device__ __forceinline__ Tile& slot() {
+    if constexpr (S >= TS_HA && S < TS_HB) return Ha[S - TS_HA];
+    else if constexpr (S >= TS_HB && S < TS_X) return Hb[S - TS_HB];
+    else if constexpr (S == TS_G) return G;
+    else {
+      static_assert(S == TS_DA, "dX tile slot");
+      return DA;
+    }
+  }
+  static __host__ __device__ constexpr int stage_of(int u) { return bwd16_unit_stage(u); }
+
+  // half hf of the 32-feature dZ tile tau (old layout): fp32 values v[4 hf .. 4 hf + 3], or the bf16x3 hi / lo dwords
+  // 2 hf, 2 hf + 1 (8 bytes each, lo 2 KiB after hi)
+  __device__ __forceinline__ void store_half(int tau, int hf, const Tile& t) {
+    if constexpr (F32) {
+      char* base = (char*)a.dz + (((wb32 * ZT_TILES + tau) * SCH + 2 * hf) << 10) + st_off;
+      store16<0>((uint4*)base, make_uint4(__float_as_uint(t.v[4 * hf]), __float_as_uint(t.v[4 * hf + 1]),
+                                          __float_as_uint(t.v[4 * hf + 2]), __float_as_uint(t.v[4 * hf + 3])));
+    } else {
+      char* base = (char*)a.dz + (((wb32 * ZT_TILES + tau) * SCH + hf) << 10) + st_off;
+      store8(base, get_dword(t.hi, 2 * hf), get_dword(t.hi, 2 * hf + 1));
+      store8(base + 2048, get_dword(t.lo, 2 * hf), get_dword(t.lo, 2 * hf + 1));
+    }
+  }
+
+  // ---- group_body hooks
+  template <int u, int t> __device__ __forceinline__ const Tile& in_tile() {
+    return slot<bwd_in_slot(stage_of(u), t)>();
+  }
+  template <int u> __device__ __forceinline__ void prefetch() {}
+  template <int u> __device__ __forceinline__ void init(Acc& acc) {
+    acc[0] = acc[1] = acc[2] = acc[3] = 0.f;
+  }
+  // part p of NP of unit u (half m & 1 of output tile j = m >> 1 of stage st): its register pairs masked by the
+  // forward's ReLU bits into the output-gradient K-block (in place); the last part stores
+  template <int u, int p> __device__ __forceinline__ void finish_part(const Acc& acc) {
+    constexpr int st = stage_of(u), mu = u - bwd16_unit_first(st), j = mu >> 1, hf = mu & 1;
+    constexpr int mg = bwd_mask_group(st);
+    constexpr int NP = finish_parts<P>();
+    constexpr int K0 = 2 * p / NP, K1 = 2 * (p + 1) / NP;
+    uint32_t w = 0xFFFFFFFFu;
+    if constexpr (mg >= 0) {
+      // value e (pair k = e >> 1, element e & 1) of this lane: old register rho = 4 (2 hf + (g >> 1)) + e of old
+      // tile j, mask bit 8 (j & 1) + (rho >> 1) + 16 (rho & 1) = [k + 16 (e & 1)] << (8 (j & 1) + 4 hf + gsh)
+      const uint32_t d = (j >> 1) == 0 ? mk[mg].x : (j >> 1) == 1 ? mk[mg].y : (j >> 1) == 2 ? mk[mg].z : mk[mg].w;
+      w = d >> ((uint32_t)(8 * (j & 1) + 4 * hf) + gsh);
+    }
+    Tile& out = slot<bwd_out_slot(st, j)>();
+    sfor<K1 - K0>([&](auto kk) {
+      constexpr int k = K0 + decltype(kk)::value;
+      const float y0 = ((w >> k) & 1u) ? acc[2 * k] : 0.f;
+      const float y1 = ((w >> (16 + k)) & 1u) ? acc[2 * k + 1] : 0.f;
+      if constexpr (F32) {
+        out.v[4 * hf + 2 * k] = y0;
+        out.v[4 * hf + 2 * k + 1] = y1;
+      } else {
+        const uint32_t hw = pack_bf16(y0, y1);
+        const uint32_t lw = pack_bf16(y0 - __uint_as_float(hw << 16), y1 - __uint_as_float(hw & 0xffff0000u));
+        set_dword8(out.hi, 2 * hf + k, hw);
+        set_dword8(out.lo, 2 * hf + k, lw);
+      }
+    });
+    if constexpr (p == NP - 1) store_half(bwd_dz_tile(st, j), hf, out);
+  }
+
+  template <int gi> __device__ __forceinline__ void step() {
+    constexpr int NG = GT::t.n;
+    if constexpr (gi + PF < NG && dma_spread<P>() == 0) fetch<gi + PF>();
+    const uint32_t sl = lds_base + (uint32_t)((gi % NSLOT) * SLOT_CAP * 1024);
+    group_body<P, 3, false, gi>(*this, lds_ptr(sl + (uint32_t)(lane * 16)));
+    constexpr int N = dma_spread<P>() > 0
+        ? handoff_vmcnt_spread<P, 3, false>(gi, [](int u) constexpr { return unit_stores(u); })
+        : handoff_vmcnt<P, 3, false>(gi, [](int i) constexpr { return group_stores(i); }, 4 * SST);
+    if constexpr (gi + 1 < NG) wait_barrier<N>();
+  }
+
+  // the seed tiles: K-block 0 of d rgb (features 0..2) and of d alpha (feature 0), element e of lane group g =
+  // feature k16_feat(g, e): lane group 0's elements 0..2 / 0
+  __device__ __forceinline__ void seed(Tile& t, float v0, float v1, float v2) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    if (g == 0) v[0] = v0, v[1] = v1, v[2] = v2;
+    if constexpr (F32) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t.v[e] = v[e];
+    } else {
+      uint32_t hw[4], lw[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        hw[k] = pack_bf16(v[2 * k], v[2 * k + 1]);
+        lw[k] = pack_bf16(v[2 * k] - __uint_as_float(hw[k] << 16), v[2 * k + 1] - __uint_as_float(hw[k] & 0xffff0000u));
+      }
+      t.hi = __builtin_bit_cast(bf16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
+      t.lo = __builtin_bit_cast(bf16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+    }
+  }
+
+  __device__ __forceinline__ void run() {
+    const float4 gr = m < a.M ? *(const float4*)(a.d_raw + m * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < MASK_GROUPS; ++i) mk[i] = *mask_slot((void*)a.masks, wb32, i, (int)lold);
+    sfor<(PF < GT::t.n ? PF : GT::t.n)>([&](auto gg) { fetch<decltype(gg)::value>(); });
+    seed(G, gr.x, gr.y, gr.z);
+    seed(DA, gr.w, 0.f, 0.f);
+    store_half(ZT_RGB, 0, G);
+    store_half(ZT_RGB, 1, G);
+    store_half(ZT_A, 0, DA);
+    store_half(ZT_A, 1, DA);
+    {
+      constexpr int N0 = [] {
+        int n = 4 * SST;
+        for (int j = 1; j < PF && j < GT::t.n; ++j) n += group_dma<P, 3, false>(j);
+        return n;
+      }();
+      wait_barrier<N0>();
+    }
+#pragma unroll
+    for (int i = 0; i < MASK_GROUPS; ++i) {
+      settle(mk[i].x);
+      settle(mk[i].y);
+      settle(mk[i].z);
+      settle(mk[i].w);
+    }
+    sfor<GT::t.n>([&](auto gg) { step<decltype(gg)::value>(); });
+  }
+};
+
+template <class P>
+using DxWaveOf = std::conditional_t<wide_kind<P>(), DxWave16<P>, DxWave<P>>;
+
 template <class P>
 __global__ void __launch_bounds__(P::WAVES * 64) dx_kernel(DxArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem_u4[];
-  DxWave<P> w(a, smem_u4);
+  DxWaveOf<P> w(a, smem_u4);
   w.run();
 }
 
@@ -2971,9 +3197,11 @@ namespace mlp {
 static_assert(NET_PARAMS < (1 << 24), "a plan entry holds a 24-bit parameter offset");
 // the packed-weight layout of a policy's forward: 32-row units (0), or the 16-row units of PBF3W (2)
 template <class P> static constexpr int fwd_layout() { return wide_kind<P>() ? 2 : 0; }
+// ... and of its dX: 32-row units (1), or the 16-row units of PF32W / PBF3W (3)
+template <class P> static constexpr int bwd_layout() { return wide_kind<P>() ? 3 : 1; }
 template <class P, class F> static void with_layout(int dir, F&& f) {  // f(integral_constant<layout>)
   if (dir == 1) {
-    if constexpr (fwd_layout<P>() != 2) f(std::integral_constant<int, 1>{});  // (PBF3W: forward only)
+    f(std::integral_constant<int, bwd_layout<P>()>{});
   } else {
     f(std::integral_constant<int, fwd_layout<P>()>{});
   }
@@ -2992,7 +3220,7 @@ static const uint32_t* pack_plan(int dir, const void* params, hipStream_t stream
     if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess || (cur != dev && hipSetDevice(dev) != hipSuccess)) return nullptr;
-    const int64_t n = total_chunks(P::CH, dir == 0 ? fwd_layout<P>() : 1) * 64;
+    const int64_t n = total_chunks(P::CH, dir == 0 ? fwd_layout<P>() : bwd_layout<P>()) * 64;
     uint32_t* p = nullptr;
     bool ok = hipMalloc(&p, (size_t)n * P::E * sizeof(uint32_t)) == hipSuccess;
     if (ok) {
@@ -3012,7 +3240,7 @@ static const uint32_t* pack_plan(int dir, const void* params, hipStream_t stream
 }
 template <class P>
 void mlp_pack_impl(const ParamPtrs& prm, int dir, char* dst, hipStream_t stream) {
-  const int64_t n = total_chunks(P::CH, dir == 0 ? fwd_layout<P>() : 1) * 64;
+  const int64_t n = total_chunks(P::CH, dir == 0 ? fwd_layout<P>() : bwd_layout<P>()) * 64;
   dim3 grid((unsigned)((n + 255) / 256));
   // the 24 parameters back to back (FusedAdam's flat buffer): the plan gather (NERF_PACK_PLAN=0: always
   // the direct pack, for A/B timing)
@@ -3055,6 +3283,17 @@ using PBF3F = std::conditional_t<NERF_BF3_WIDE != 0, PBF3W, PBF3>;
 #endif
 using PF32T = std::conditional_t<NERF_F32_WIDE != 0, PF32W, PF32>;
 [[maybe_unused]] constexpr int64_t F32W_PACK_OFF = NERF_F32_WIDE ? total_chunks(PF32::CH, 0) * 1024 : 0;
+// The dX of fp32 and bf16x3: the wide 16x16 kernels (DxWave16 over 16-row units, round 6) or, with
+// -DNERF_F32_WIDE_DX=0 / -DNERF_BF3_WIDE_DX=0, the 32x32 ones; their W^T packs follow (bwd_layout).  The dZ they
+// store is the same old-layout tile-block list either way (the dW is unchanged).
+#ifndef NERF_F32_WIDE_DX
+#define NERF_F32_WIDE_DX 1
+#endif
+#ifndef NERF_BF3_WIDE_DX
+#define NERF_BF3_WIDE_DX 1
+#endif
+using PF32X = std::conditional_t<NERF_F32_WIDE_DX != 0, PF32W, PF32>;
+using PBF3X = std::conditional_t<NERF_BF3_WIDE_DX != 0, PBF3W, PBF3>;
 // bf16x3 forward, bf16 (hi-half) stores for the bf16 backward
 void mlp_fwd_train_half_impl(const FwdArgs& a, hipStream_t stream);
 #if defined(NERF_MLP_PREC) && NERF_MLP_PREC == 2 && (!defined(NERF_MLP_PART) || NERF_MLP_PART == 4)
@@ -3099,18 +3338,16 @@ void mlp_dw_impl(const DwArgs& w, dim3 grid, hipStream_t stream) {
   NERF_MLP_I_FWDT(EXT, P) NERF_MLP_I_FWDI(EXT, P) NERF_MLP_I_FWDD(EXT, P) NERF_MLP_I_FWDP(EXT, P)
 #if !defined(NERF_MLP_PREC)
 NERF_MLP_IMPLS(extern, PF32)
-#if NERF_F32_WIDE
 NERF_MLP_I_FWDT(extern, PF32W)
 NERF_MLP_I_PACK(extern, PF32W)
-#endif
+NERF_MLP_I_DX(extern, PF32W)
+NERF_MLP_I_DX(extern, PBF3W)
 NERF_MLP_IMPLS(extern, PBF16)
 NERF_MLP_I_PACK(extern, PBF3)  // bf16x3: the W^T pack, dX, dW (+ the forward pack when not wide)
 NERF_MLP_I_DX(extern, PBF3)
 NERF_MLP_I_DW(extern, PBF3)
 NERF_MLP_FWDS(extern, PBF3F)
-#if NERF_BF3_WIDE
 NERF_MLP_I_PACK(extern, PBF3W)
-#endif
 NERF_MLP_I_FWDI(extern, PBF6)  // bf16x6: the inference forward and its pack only
 NERF_MLP_I_PACK(extern, PBF6)
 #elif NERF_MLP_PREC == 3
@@ -3150,13 +3387,20 @@ NERF_MLP_I_FWDD(, NERF_PP_FWD)
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 6
 NERF_MLP_I_FWDP(, NERF_PP_FWD)
 #endif
+#if NERF_MLP_PREC == 0
+#define NERF_PP_DX PF32X  // (the fp32 dX: PF32W unless NERF_F32_WIDE_DX=0)
+#elif NERF_MLP_PREC == 2
+#define NERF_PP_DX PBF3X  // (the bf16x3 dX: PBF3W unless NERF_BF3_WIDE_DX=0)
+#else
+#define NERF_PP_DX NERF_PP
+#endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 2
-NERF_MLP_I_DX(, NERF_PP)
+NERF_MLP_I_DX(, NERF_PP_DX)
 NERF_MLP_I_PACK(, NERF_PP)
-#if NERF_MLP_PREC == 2 && NERF_BF3_WIDE
+#if NERF_MLP_PREC == 2 && (NERF_BF3_WIDE || NERF_BF3_WIDE_DX)
 NERF_MLP_I_PACK(, PBF3W)
 #endif
-#if NERF_MLP_PREC == 0 && NERF_F32_WIDE
+#if NERF_MLP_PREC == 0 && (NERF_F32_WIDE || NERF_F32_WIDE_DX)
 NERF_MLP_I_PACK(, PF32W)
 #endif
 #endif
@@ -3189,6 +3433,8 @@ int64_t nerf_mlp_packed_bytes(int dtype, int dir) {
   if (p == 2 && dir == 0) return total_chunks(PBF3F::CH, fwd_layout<PBF3F>()) * 1024;  // (the wide bf16x3 forward)
   if (p == 0 && dir == 0 && NERF_F32_WIDE)  // PF32's units, then PF32W's (the training forward)
     return F32W_PACK_OFF + total_chunks(PF32W::CH, fwd_layout<PF32W>()) * 1024;
+  if (p == 0 && dir == 1) return total_chunks(PF32X::CH, bwd_layout<PF32X>()) * 1024;  // (the fp32 dX)
+  if (p == 2 && dir == 1) return total_chunks(PBF3X::CH, bwd_layout<PBF3X>()) * 1024;  // (the bf16x3 dX)
   return total_chunks(p == 1 ? PBF16::CH : PF32::CH, dir) * 1024;  // bf16x3: CH 4 as fp32
 }
 
@@ -3218,13 +3464,14 @@ int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void*
     if (!dst) continue;
     const int p = dir == 0 ? fwd_prec(dtype) : bwd_prec(dtype);
     if (p == 4) mlp_pack_impl<PBF6>(prm, dir, (char*)dst, stream);
+    else if (p == 0 && dir == 1) mlp_pack_impl<PF32X>(prm, dir, (char*)dst, stream);
     else if (p == 0) {
       mlp_pack_impl<PF32>(prm, dir, (char*)dst, stream);
       if (dir == 0 && NERF_F32_WIDE) mlp_pack_impl<PF32T>(prm, dir, (char*)dst + F32W_PACK_OFF, stream);
     }
     else if (p == 1) mlp_pack_impl<PBF16>(prm, dir, (char*)dst, stream);
     else if (dir == 0) mlp_pack_impl<PBF3F>(prm, dir, (char*)dst, stream);
-    else mlp_pack_impl<PBF3>(prm, dir, (char*)dst, stream);
+    else mlp_pack_impl<PBF3X>(prm, dir, (char*)dst, stream);
     if (int e = check_launch("nerf_mlp_pack")) return e;
   }
   return 0;
@@ -3396,9 +3643,9 @@ int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64
   NERF_REQUIRE(packed_bwd && d_raw && masks && dz, "nerf_mlp_bwd_dx: null pointer");
   const int64_t ldm = nerf_mlp_padded_samples(M);
   DxArgs x{(const char*)packed_bwd, d_raw, M, ldm / 32, masks, dz};
-  if (dtype == 0) mlp_dx_impl<PF32>(x, ldm, stream);
+  if (dtype == 0) mlp_dx_impl<PF32X>(x, ldm, stream);
   else if (dtype == 1) mlp_dx_impl<PBF16>(x, ldm, stream);
-  else mlp_dx_impl<PBF3>(x, ldm, stream);
+  else mlp_dx_impl<PBF3X>(x, ldm, stream);
   return check_launch("nerf_mlp_bwd_dx");
 }
 

@@ -163,8 +163,30 @@ __host__ __device__ constexpr int fwd16_out_row0(int L, int m) { return (L == LF
 __host__ __device__ constexpr int fwd16_out_valid(int L, int m) {
   return (L == LFA && m == 16) ? 1 : L == LRGB ? 3 : 16;
 }
-constexpr int NUNIT_MAX = NUNIT_FWD16;  // the largest unit table (forward 78, dX 76, 16-row forward 154)
-static_assert(NUNIT_FWD16 > NUNIT_FWD && NUNIT_FWD16 > NUNIT_BWD, "NUNIT_MAX");
+// 16-row dX units (round 6: the wide dX of PF32W / PBF3W): unit = one 16-row half m & 1 of output tile m >> 1 of a
+// dX stage; its input is the stage's list of 32-feature K-blocks, in the same permuted order (k16_feat)
+__host__ __device__ constexpr int bwd16_out_tiles(int s) { return 2 * bwd_out_tiles(s); }
+constexpr int NUNIT_BWD16 = 8 + 16 * 9;  // 152
+__host__ __device__ constexpr int bwd16_unit_first(int s) {
+  int u = 0;
+  for (int k = 0; k < s; ++k) u += bwd16_out_tiles(k);
+  return u;
+}
+__host__ __device__ constexpr int bwd16_unit_stage(int u) {
+  int s = 0;
+  while (s < NBSTAGE - 1 && u >= bwd16_unit_first(s + 1)) ++s;
+  return s;
+}
+__host__ __device__ constexpr int bwd16_unit_tiles(int u) { return bwd_in_tiles(bwd16_unit_stage(u)); }
+__host__ __device__ constexpr int bwd16_unit_tile_off(int u) {
+  int o = 0;
+  for (int k = 0; k < u; ++k) o += bwd16_unit_tiles(k);
+  return o;
+}
+constexpr int BWD16_TILES = bwd16_unit_tile_off(NUNIT_BWD16);
+
+constexpr int NUNIT_MAX = NUNIT_FWD16;  // the largest unit table (forward 78, dX 76, 16-row forward 154, dX 152)
+static_assert(NUNIT_FWD16 > NUNIT_FWD && NUNIT_FWD16 > NUNIT_BWD && NUNIT_FWD16 >= NUNIT_BWD16, "NUNIT_MAX");
 
 // Training stores, "fragment-native": a stored tensor is a list of 32-feature tiles; tile
 // tau of 32-sample block b occupies one tile-block of CH KiB at ((tau * nblk + b) * CH + c)

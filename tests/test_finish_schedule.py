@@ -27,7 +27,8 @@ CASES = [("PF32", 0, "false"), ("PF32", 0, "true"), ("PF32", 1, "false"),
          ("PBF16", 0, "false"), ("PBF16", 0, "true"), ("PBF16", 1, "false"),
          ("PBF3", 0, "false"), ("PBF3", 0, "true"), ("PBF3", 1, "false"), ("PBF6", 0, "false"),
          ("PBF3W", 2, "false"), ("PBF3W", 2, "true"),  # (the wide bf16x3 forward: 16-row units)
-         ("PF32W", 2, "false")]  # (the wide fp32 training forward)
+         ("PF32W", 2, "false"),  # (the wide fp32 training forward)
+         ("PF32W", 3, "false"), ("PBF3W", 3, "false")]  # (the wide dX: 16-row W^T units)
 
 
 def _violations(tmp, defines):

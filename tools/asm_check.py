@@ -29,7 +29,8 @@ KERNELS = [f"fwd_kernel<nerf::mlp::{p}, {a}>" for p in ("PF32", "PBF16", "PBF3W"
            for a in ("true, false, false", "false, false, false", "false, true, false", "false, false, true")] + \
           ["fwd_kernel<nerf::mlp::PBF3W, true, false, false, true>", "fwd_kernel<nerf::mlp::PBF6, false, false, false>",
            "fwd_kernel<nerf::mlp::PF32W, true, false, false>"] + \
-          [f"{k}_kernel<nerf::mlp::{p}>" for k in ("dx", "dw") for p in ("PF32", "PBF16", "PBF3")]
+          [f"{k}_kernel<nerf::mlp::{p}>" for k in ("dx", "dw") for p in ("PF32", "PBF16", "PBF3")] + \
+          ["dx_kernel<nerf::mlp::PF32W>", "dx_kernel<nerf::mlp::PBF3W>"]  # (the wide dX, round 6)
 
 
 def build_asm(tmp, kernels=None):
