@@ -47,7 +47,7 @@ __device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
 // ------------------------------------------------------------------------------------
 // precision policies
 // ------------------------------------------------------------------------------------
-enum PKind { K_F32 = 0, K_BF16 = 1, K_BF16X3 = 2, K_BF16X6 = 3, K_BF16X3W = 4, K_F32W = 5 };
+enum PKind { K_F32 = 0, K_BF16 = 1, K_BF16X3 = 2, K_BF16X6 = 3, K_BF16X3W = 4, K_F32W = 5, K_BF16W = 6 };
 
 struct PF32 {
   static constexpr int KIND = K_F32;
@@ -361,7 +361,31 @@ struct PF32W {
   static __host__ __device__ constexpr int feat16(int c, int g, int e) { return 16 * c + 4 * g + e; }
   static __host__ __device__ constexpr int part16(int) { return 0; }
 };
-template <class P> __host__ __device__ constexpr bool wide_kind() { return P::KIND == K_BF16X3W || P::KIND == K_F32W; }
+// The wide bf16 dX (round 6, PBF16W): the bf16 dX of the bf16 and bf16x3f tiers on v_mfma_f32_16x16x32_bf16 over the
+// 16-row W^T units -- PBF3W's layout with the hi half only (one 1 KiB chunk per K-block).
+struct PBF16W {
+  static constexpr int KIND = K_BF16W;
+  using Acc = f32x4;
+  static constexpr int SPW = 16;
+  static constexpr int CH = 1;
+  static constexpr int E = 8;
+  static constexpr int WAVES = 8;
+  static constexpr int ESIZE = 2;
+  static constexpr int SPL = 8;
+  static constexpr int PE = 0;
+  using Store = __bf16;
+  struct Tile { bf16x8 hi; };
+  static __device__ __forceinline__ f32x4 mma(uint4 a, const Tile& b, int, f32x4 acc) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), b.hi, acc, 0, 0, 0);
+  }
+  static __host__ __device__ constexpr int rho_of(int, int e) { return e; }
+  static __device__ __forceinline__ Store cvt_c(float x, int) { return (__bf16)x; }
+  static __host__ __device__ constexpr int feat16(int, int g, int e) { return k16_feat(g, e); }
+  static __host__ __device__ constexpr int part16(int) { return 0; }
+};
+template <class P> __host__ __device__ constexpr bool wide_kind() {
+  return P::KIND == K_BF16X3W || P::KIND == K_F32W || P::KIND == K_BF16W;
+}
 
 // ReLU-mask bit of accumulator register rho of a tile: the tile's 16 bits sit at positions
 // (rho >> 1) + 16 (rho & 1) of a dword (bf16 pair k = registers 2k, 2k+1 -> bits k, 16 + k),
@@ -819,6 +843,11 @@ template <class P> __host__ __device__ constexpr int prefetch_depth() {
   return P::KIND == K_F32 ? NERF_PREFETCH_F32 : P::KIND == K_F32W ? NERF_PREFETCH_F32W : NERF_PREFETCH_BF16;  // a bf16 / bf16x3 step is 1-2 short MFMAs
 }
 constexpr int FINISH_DELAY = NERF_FINISH_DELAY;
+// (the wide bf16 dX, one chunk per K-block: the dX stage bV reads bRGB's last output K-block at its step 3, so its
+// finish runs 1 step into bV's first unit -- with 3 FinishSchedule refuses the build)
+#ifndef NERF_FINISH_DELAY_BF16W
+#define NERF_FINISH_DELAY_BF16W 1
+#endif
 
 // Cross-group finish: the last unit of a group is finished after the barrier.  Not in the
 // bf16x3 forward: a finished accumulator carried over the barrier (plus the hi / lo split of
@@ -869,10 +898,13 @@ __host__ __device__ constexpr bool finished_in_group(int g, int u) {
 #ifndef NERF_FINISH_PARTS_F32W
 #define NERF_FINISH_PARTS_F32W 2
 #endif
+#ifndef NERF_FINISH_PARTS_BF16W
+#define NERF_FINISH_PARTS_BF16W 2
+#endif
 template <class P> __host__ __device__ constexpr int finish_parts() {
   return P::KIND == K_F32 ? NERF_FINISH_PARTS_F32 : P::KIND == K_BF16 ? NERF_FINISH_PARTS_BF16
        : P::KIND == K_BF16X3W ? NERF_FINISH_PARTS_BF3W : P::KIND == K_F32W ? NERF_FINISH_PARTS_F32W
-       : NERF_FINISH_PARTS_BF3;
+       : P::KIND == K_BF16W ? NERF_FINISH_PARTS_BF16W : NERF_FINISH_PARTS_BF3;
 }
 // DMA spread.  0: the next group's LDS-DMA pieces (up to 18 per wave, ~7 instructions each)
 // are issued as one burst at the group's start; S > 0: piece i at step i (NS / S) / NF of the
@@ -892,9 +924,13 @@ template <class P> __host__ __device__ constexpr int finish_parts() {
 #ifndef NERF_DMA_SPREAD_F32W
 #define NERF_DMA_SPREAD_F32W 3
 #endif
+#ifndef NERF_DMA_SPREAD_BF16W
+#define NERF_DMA_SPREAD_BF16W 3
+#endif
 template <class P> __host__ __device__ constexpr int dma_spread() {
   return PF != 1 ? 0 : P::KIND == K_F32 ? NERF_DMA_SPREAD_F32 : P::KIND == K_BF16 ? NERF_DMA_SPREAD_BF16
-       : P::KIND == K_BF16X3W ? NERF_DMA_SPREAD_BF3W : P::KIND == K_F32W ? NERF_DMA_SPREAD_F32W : NERF_DMA_SPREAD_BF3;
+       : P::KIND == K_BF16X3W ? NERF_DMA_SPREAD_BF3W : P::KIND == K_F32W ? NERF_DMA_SPREAD_F32W
+       : P::KIND == K_BF16W ? NERF_DMA_SPREAD_BF16W : NERF_DMA_SPREAD_BF3;
 }
 
 // step (in group g) at which part p of unit u's finish is issued, or -1 when u is not
@@ -910,7 +946,7 @@ __host__ __device__ constexpr int part_step(int g, int u, int p) {
   int start = 0;
   for (int j = 0; j < js; ++j) start += unit_tiles<DIR>(G.u0 + j) * P::CH;
   const int len = unit_tiles<DIR>(G.u0 + js) * P::CH;
-  const int d = FINISH_DELAY + p;
+  const int d = (P::KIND == K_BF16W ? NERF_FINISH_DELAY_BF16W : FINISH_DELAY) + p;
   return start + (d < len - 1 ? d : len - 1);
 }
 // step (in group g) of the i-th of the next group's NF DMA pieces (dma_spread > 0)
@@ -2284,11 +2320,11 @@ template <class P>
 struct DxWave16 {
   using Tile = typename P::Tile;
   using Acc = f32x4;
-  static constexpr bool F32 = P::KIND == K_F32W;
-  static_assert(wide_kind<P>(), "DxWave16: PF32W or PBF3W");
+  static constexpr bool F32 = P::KIND == K_F32W, B16 = P::KIND == K_BF16W;
+  static_assert(wide_kind<P>(), "DxWave16: PF32W, PBF3W or PBF16W");
   static constexpr int CH = P::CH;
-  static constexpr int SCH = 4;             // chunks of a stored dZ tile-block (fp32, or bf16x3 hi + lo)
-  static constexpr int SST = F32 ? 1 : 2;   // stores per output tile: one 16-byte (fp32) or hi + lo 8-byte
+  static constexpr int SCH = B16 ? 2 : 4;   // chunks of a stored dZ tile-block (fp32, bf16x3 hi + lo, bf16)
+  static constexpr int SST = B16 || F32 ? 1 : 2;  // stores per output tile: 16-byte (fp32), hi [+ lo] 8-byte
   using GT = GroupTable<3, false, P::CH>;
   static_assert(finish_schedule_violation<P, 3, false>() == 0,
                 "finish placement (NERF_FINISH_PARTS_* / NERF_FINISH_DELAY) reads a tile pair before its finish part "
@@ -2356,7 +2392,7 @@ struct DxWave16 {
     } else {
       char* base = (char*)a.dz + (((wb32 * ZT_TILES + tau) * SCH + hf) << 10) + st_off;
       store8(base, get_dword(t.hi, 2 * hf), get_dword(t.hi, 2 * hf + 1));
-      store8(base + 2048, get_dword(t.lo, 2 * hf), get_dword(t.lo, 2 * hf + 1));
+      if constexpr (!B16) store8(base + 2048, get_dword(t.lo, 2 * hf), get_dword(t.lo, 2 * hf + 1));
     }
   }
 
@@ -2390,6 +2426,8 @@ struct DxWave16 {
       if constexpr (F32) {
         out.v[4 * hf + 2 * k] = y0;
         out.v[4 * hf + 2 * k + 1] = y1;
+      } else if constexpr (B16) {
+        set_dword8(out.hi, 2 * hf + k, pack_bf16(y0, y1));
       } else {
         const uint32_t hw = pack_bf16(y0, y1);
         const uint32_t lw = pack_bf16(y0 - __uint_as_float(hw << 16), y1 - __uint_as_float(hw & 0xffff0000u));
@@ -2429,7 +2467,7 @@ struct DxWave16 {
         lw[k] = pack_bf16(v[2 * k] - __uint_as_float(hw[k] << 16), v[2 * k + 1] - __uint_as_float(hw[k] & 0xffff0000u));
       }
       t.hi = __builtin_bit_cast(bf16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
-      t.lo = __builtin_bit_cast(bf16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+      if constexpr (!B16) t.lo = __builtin_bit_cast(bf16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
     }
   }
 
@@ -3292,7 +3330,14 @@ using PF32T = std::conditional_t<NERF_F32_WIDE != 0, PF32W, PF32>;
 #ifndef NERF_BF3_WIDE_DX
 #define NERF_BF3_WIDE_DX 1
 #endif
+// (the bf16 dX stays the 32x32 kernel: the wide one, PBF16W, reads a 1 KiB weight chunk per single 16x16x32 MFMA --
+// twice the LDS bytes per flop of the 32x32 kernel's, which already ran two waves per SIMD -- and measured slower,
+// bf16 dX 0.596 -> 0.747 ms, bf16x3f's 0.564 -> 0.724, profiles/r6/wide_dx_bf16_ab.json; -DNERF_BF16_WIDE_DX=1)
+#ifndef NERF_BF16_WIDE_DX
+#define NERF_BF16_WIDE_DX 0
+#endif
 using PF32X = std::conditional_t<NERF_F32_WIDE_DX != 0, PF32W, PF32>;
+using PBF16X = std::conditional_t<NERF_BF16_WIDE_DX != 0, PBF16W, PBF16>;  // (the bf16 / bf16x3f dX)
 using PBF3X = std::conditional_t<NERF_BF3_WIDE_DX != 0, PBF3W, PBF3>;
 // bf16x3 forward, bf16 (hi-half) stores for the bf16 backward
 void mlp_fwd_train_half_impl(const FwdArgs& a, hipStream_t stream);
@@ -3342,6 +3387,8 @@ NERF_MLP_I_FWDT(extern, PF32W)
 NERF_MLP_I_PACK(extern, PF32W)
 NERF_MLP_I_DX(extern, PF32W)
 NERF_MLP_I_DX(extern, PBF3W)
+NERF_MLP_I_DX(extern, PBF16W)
+NERF_MLP_I_PACK(extern, PBF16W)
 NERF_MLP_IMPLS(extern, PBF16)
 NERF_MLP_I_PACK(extern, PBF3)  // bf16x3: the W^T pack, dX, dW (+ the forward pack when not wide)
 NERF_MLP_I_DX(extern, PBF3)
@@ -3391,6 +3438,8 @@ NERF_MLP_I_FWDP(, NERF_PP_FWD)
 #define NERF_PP_DX PF32X  // (the fp32 dX: PF32W unless NERF_F32_WIDE_DX=0)
 #elif NERF_MLP_PREC == 2
 #define NERF_PP_DX PBF3X  // (the bf16x3 dX: PBF3W unless NERF_BF3_WIDE_DX=0)
+#elif NERF_MLP_PREC == 1
+#define NERF_PP_DX PBF16X  // (the bf16 dX: PBF16W unless NERF_BF16_WIDE_DX=0)
 #else
 #define NERF_PP_DX NERF_PP
 #endif
@@ -3402,6 +3451,9 @@ NERF_MLP_I_PACK(, PBF3W)
 #endif
 #if NERF_MLP_PREC == 0 && (NERF_F32_WIDE || NERF_F32_WIDE_DX)
 NERF_MLP_I_PACK(, PF32W)
+#endif
+#if NERF_MLP_PREC == 1 && NERF_BF16_WIDE_DX
+NERF_MLP_I_PACK(, PBF16W)
 #endif
 #endif
 #if !defined(NERF_MLP_PART) || NERF_MLP_PART == 3
@@ -3435,6 +3487,7 @@ int64_t nerf_mlp_packed_bytes(int dtype, int dir) {
     return F32W_PACK_OFF + total_chunks(PF32W::CH, fwd_layout<PF32W>()) * 1024;
   if (p == 0 && dir == 1) return total_chunks(PF32X::CH, bwd_layout<PF32X>()) * 1024;  // (the fp32 dX)
   if (p == 2 && dir == 1) return total_chunks(PBF3X::CH, bwd_layout<PBF3X>()) * 1024;  // (the bf16x3 dX)
+  if (p == 1 && dir == 1) return total_chunks(PBF16X::CH, bwd_layout<PBF16X>()) * 1024;  // (the bf16 dX)
   return total_chunks(p == 1 ? PBF16::CH : PF32::CH, dir) * 1024;  // bf16x3: CH 4 as fp32
 }
 
@@ -3469,6 +3522,7 @@ int nerf_mlp_pack(const float* const* params, int dtype, void* packed_fwd, void*
       mlp_pack_impl<PF32>(prm, dir, (char*)dst, stream);
       if (dir == 0 && NERF_F32_WIDE) mlp_pack_impl<PF32T>(prm, dir, (char*)dst + F32W_PACK_OFF, stream);
     }
+    else if (p == 1 && dir == 1) mlp_pack_impl<PBF16X>(prm, dir, (char*)dst, stream);
     else if (p == 1) mlp_pack_impl<PBF16>(prm, dir, (char*)dst, stream);
     else if (dir == 0) mlp_pack_impl<PBF3F>(prm, dir, (char*)dst, stream);
     else mlp_pack_impl<PBF3X>(prm, dir, (char*)dst, stream);
@@ -3644,7 +3698,7 @@ int nerf_mlp_bwd_dx(const void* packed_bwd, int dtype, const float* d_raw, int64
   const int64_t ldm = nerf_mlp_padded_samples(M);
   DxArgs x{(const char*)packed_bwd, d_raw, M, ldm / 32, masks, dz};
   if (dtype == 0) mlp_dx_impl<PF32X>(x, ldm, stream);
-  else if (dtype == 1) mlp_dx_impl<PBF16>(x, ldm, stream);
+  else if (dtype == 1) mlp_dx_impl<PBF16X>(x, ldm, stream);
   else mlp_dx_impl<PBF3X>(x, ldm, stream);
   return check_launch("nerf_mlp_bwd_dx");
 }
@@ -3700,8 +3754,8 @@ int nerf_mlp_bwd(const void* packed_bwd, int dtype, const float* d_raw, int64_t 
 // Knob policy (round 6).  Schedule knobs -- NERF_FINISH_PARTS_*, NERF_FINISH_DELAY, NERF_PREFETCH_*,
 // NERF_DMA_SPREAD_*, NERF_GROUP_ACROSS -- may take any value: every placement they produce is proven at compile
 // time (FinishSchedule's static_assert in FwdWave / FwdWave16 / DxWave; the hand-off vmcnt counts are computed
-// from the same tables and tools/asm_check.py checks them on the emitted code).  NERF_BF3_WIDE selects
-// between two verified bf16x3 forwards.  NERF_DIAG_* are diagnostic builds only (results meaningless).  Every other tuning
+// from the same tables and tools/asm_check.py checks them on the emitted code).  NERF_BF3_WIDE and NERF_*_WIDE_DX
+// select between verified kernels (below).  NERF_DIAG_* are diagnostic builds only (results meaningless).  Every other tuning
 // knob is pinned to the value the tests verified: building another value fails here.
 // ------------------------------------------------------------------------------------
 #define NERF_PINNED(K, V) static_assert((K) == (V), #K ": only the verified value " #V " is allowed (mlp.hip knob policy)");
@@ -3723,5 +3777,11 @@ NERF_PINNED(NERF_DW_COST_TABLE_BF, 1)
 #endif
 #if defined(NERF_BF3_WIDE)
 static_assert(NERF_BF3_WIDE == 0 || NERF_BF3_WIDE == 1, "NERF_BF3_WIDE: 0 (32x32 bf16x3 forward) or 1 (wide)");
+// (the other kernel selectors: NERF_F32_WIDE -- the wide fp32 training forward, opt-in, off the fp32 gradient
+// contract; NERF_F32_WIDE_DX / NERF_BF3_WIDE_DX -- the wide dX, on; NERF_BF16_WIDE_DX -- the wide bf16 dX, opt-in,
+// slower; each 0 or 1, every one of the kernels they select compiles under FinishSchedule and tools/asm_check.py)
+static_assert((NERF_F32_WIDE == 0 || NERF_F32_WIDE == 1) && (NERF_F32_WIDE_DX == 0 || NERF_F32_WIDE_DX == 1) &&
+                  (NERF_BF3_WIDE_DX == 0 || NERF_BF3_WIDE_DX == 1) && (NERF_BF16_WIDE_DX == 0 || NERF_BF16_WIDE_DX == 1),
+              "NERF_*_WIDE*: 0 or 1");
 #endif
 #undef NERF_PINNED

@@ -24,7 +24,7 @@ def test_mlp_kernels_handoffs_and_registers(capsys):
     # every MLP kernel the library builds (round 6: also the inference, density-only and persistent
     # forwards of every precision -- the render, march and bake paths -- not only the training kernels)
     kernels = asm_check.KERNELS
-    assert len(kernels) == 23  # (+ the wide fp32 training forward PF32W and the wide dX of fp32 / bf16x3)
+    assert len(kernels) == 24  # (+ the wide fp32 training forward PF32W and the wide dX of fp32 / bf16x3 / bf16)
     with tempfile.TemporaryDirectory() as tmp:
         asm = asm_check.build_asm(tmp, kernels)
     asm_check.check(asm)
@@ -50,5 +50,6 @@ def test_mlp_kernels_handoffs_and_registers(capsys):
                  "fwd_kernelINS0_5PBF3WELb1ELb0ELb0ELb0E", "dx_kernelINS0_4PBF3", "dx_kernelINS0_5PBF16",
                  "fwd_kernelINS0_5PBF3WELb1ELb0ELb0ELb1E", "fwd_kernelINS0_4PBF6ELb0ELb0ELb0E",
                  "fwd_kernelINS0_5PBF3WELb0ELb1ELb0ELb0E", "fwd_kernelINS0_4PF32ELb0ELb0ELb1ELb0E",
-                 "fwd_kernelINS0_5PF32WELb1ELb0ELb0ELb0E", "dx_kernelINS0_5PF32W", "dx_kernelINS0_5PBF3W"):
+                 "fwd_kernelINS0_5PF32WELb1ELb0ELb0ELb0E", "dx_kernelINS0_5PF32W", "dx_kernelINS0_5PBF3W",
+                 "dx_kernelINS0_6PBF16W"):
         assert re.search(name + r".*counted_waits=\d+ unsafe=0", out), "\n" + out

@@ -28,7 +28,7 @@ CASES = [("PF32", 0, "false"), ("PF32", 0, "true"), ("PF32", 1, "false"),
          ("PBF3", 0, "false"), ("PBF3", 0, "true"), ("PBF3", 1, "false"), ("PBF6", 0, "false"),
          ("PBF3W", 2, "false"), ("PBF3W", 2, "true"),  # (the wide bf16x3 forward: 16-row units)
          ("PF32W", 2, "false"),  # (the wide fp32 training forward)
-         ("PF32W", 3, "false"), ("PBF3W", 3, "false")]  # (the wide dX: 16-row W^T units)
+         ("PF32W", 3, "false"), ("PBF3W", 3, "false"), ("PBF16W", 3, "false")]  # (the wide dX: 16-row W^T units)
 
 
 def _violations(tmp, defines):
@@ -41,7 +41,7 @@ def _violations(tmp, defines):
             f.write(f'  printf("%d\\n", finish_schedule_violation<{p}, {d}, {dens}>());\n')
         f.write("}\n")
     exe = os.path.join(tmp, "sched")
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O0", "-std=c++17", f"-I{ROOT}/include", *defines, src, "-o", exe],
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O0", "-std=c++17", "-fconstexpr-steps=33554432", f"-I{ROOT}/include", *defines, src, "-o", exe],
                    check=True, capture_output=True)
     out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
     return {c: int(v) for c, v in zip(CASES, out)}
@@ -69,10 +69,10 @@ def test_unsound_placement_fails_to_compile():
         with open(src, "w") as f:
             f.write(f'#define NERF_MLP_DEVICE_ONLY\n#include "{MLP}"\n')
             f.write("template __global__ void nerf::mlp::dx_kernel<nerf::mlp::PBF16>(nerf::mlp::DxArgs);\n")
-        bad = subprocess.run([HIPCC, "--offload-arch=gfx950", "-std=c++17", f"-I{ROOT}/include", "--cuda-device-only",
+        bad = subprocess.run([HIPCC, "--offload-arch=gfx950", "-std=c++17", "-fconstexpr-steps=33554432", f"-I{ROOT}/include", "--cuda-device-only",
                               "-fsyntax-only", "-DNERF_FINISH_PARTS_BF16=8", src], capture_output=True, text=True)
         assert bad.returncode != 0 and "finish placement" in bad.stderr, bad.stderr[-2000:]
-        good = subprocess.run([HIPCC, "--offload-arch=gfx950", "-std=c++17", f"-I{ROOT}/include", "--cuda-device-only",
+        good = subprocess.run([HIPCC, "--offload-arch=gfx950", "-std=c++17", "-fconstexpr-steps=33554432", f"-I{ROOT}/include", "--cuda-device-only",
                                "-fsyntax-only", "-DNERF_FINISH_PARTS_BF16=2", src], capture_output=True, text=True)
         assert good.returncode == 0, good.stderr[-2000:]
 
@@ -84,6 +84,6 @@ def test_pinned_knobs_refuse_unverified_values():
         with open(src, "w") as f:
             f.write(f'#define NERF_MLP_DEVICE_ONLY\n#include "{MLP}"\n')
         for knob in ("-DNERF_DW_NBUF_BF16=2", "-DNERF_PACKED_MASK=0", "-DNERF_DMA_LEAN=0", "-DNERF_KEEP_PE_BF3=0"):
-            bad = subprocess.run([HIPCC, "--offload-arch=gfx950", "-std=c++17", f"-I{ROOT}/include",
+            bad = subprocess.run([HIPCC, "--offload-arch=gfx950", "-std=c++17", "-fconstexpr-steps=33554432", f"-I{ROOT}/include",
                                   "--cuda-device-only", "-fsyntax-only", knob, src], capture_output=True, text=True)
             assert bad.returncode != 0 and "knob policy" in bad.stderr, (knob, bad.stderr[-1500:])

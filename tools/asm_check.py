@@ -30,7 +30,7 @@ KERNELS = [f"fwd_kernel<nerf::mlp::{p}, {a}>" for p in ("PF32", "PBF16", "PBF3W"
           ["fwd_kernel<nerf::mlp::PBF3W, true, false, false, true>", "fwd_kernel<nerf::mlp::PBF6, false, false, false>",
            "fwd_kernel<nerf::mlp::PF32W, true, false, false>"] + \
           [f"{k}_kernel<nerf::mlp::{p}>" for k in ("dx", "dw") for p in ("PF32", "PBF16", "PBF3")] + \
-          ["dx_kernel<nerf::mlp::PF32W>", "dx_kernel<nerf::mlp::PBF3W>"]  # (the wide dX, round 6)
+          ["dx_kernel<nerf::mlp::PF32W>", "dx_kernel<nerf::mlp::PBF3W>", "dx_kernel<nerf::mlp::PBF16W>"]  # (wide dX, r6)
 
 
 def build_asm(tmp, kernels=None):
@@ -46,7 +46,8 @@ def build_asm(tmp, kernels=None):
             f.write(f'#include "{ROOT}/nerf-replication_amd/csrc/mlp.hip"\n')
             f.write(f"template __global__ void nerf::mlp::{k}{args[k[:3]]};\n")
         extra = os.environ.get("NERF_ASM_EXTRA", "").split()  # variant -D flags (tools/build_variants.sh)
-        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", *extra,
+        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                                       "-fconstexpr-steps=33554432", *extra,
                                        f"-I{ROOT}/include", "--cuda-device-only", "-S", src, "-o",
                                        os.path.join(tmp, f"k{i}.s")], cwd=tmp, stdout=subprocess.DEVNULL,
                                       stderr=subprocess.DEVNULL))

@@ -1,6 +1,6 @@
 """The wide dX (round 6, DxWave16: PF32W / PBF3W) against the 32x32 one (diagnostic; GPU).
 
-    python tools/dx_compare.py --libs old.so,new.so [--dtype fp32|bf16x3] [--M 524288]
+    python tools/dx_compare.py --libs old.so,new.so [--dtype fp32|bf16x3|bf16|bf16x3f] [--M 524288]
 
 One training forward (the first build) gives the masks and activations; each build packs its own W^T layout and runs
 its dX on those masks and one d_raw, twice.  Reports: the new dX bit-identical run to run; dZ of the two builds
@@ -31,9 +31,12 @@ def dz_values(dz, nblk, fp32):
     if fp32:
         v = dz.view(torch.float32).view(nblk, ZT_TILES, 4, 64, 4).permute(0, 1, 3, 2, 4).reshape(nblk, ZT_TILES, 64, 16)
         return v.double()
-    b = dz.view(torch.int16).view(nblk, ZT_TILES, 4, 64, 8)
+    nch = dz.numel() // (nblk * ZT_TILES * 1024)  # 4 (bf16x3: hi, lo) or 2 (bf16)
+    b = dz.view(torch.int16).view(nblk, ZT_TILES, nch, 64, 8)
     f = (b.to(torch.int32) << 16).view(torch.float32).double()  # bf16 -> fp32 exactly
     hi = f[:, :, 0:2].permute(0, 1, 3, 2, 4).reshape(nblk, ZT_TILES, 64, 16)
+    if nch == 2:
+        return hi
     lo = f[:, :, 2:4].permute(0, 1, 3, 2, 4).reshape(nblk, ZT_TILES, 64, 16)
     return hi + lo
 
