@@ -25,6 +25,9 @@ LABELS = {
     "fwd_kernel<nerf::mlp::PBF3, true, false,": "mlp_fwd_train",
     "fwd_kernel<nerf::mlp::PBF3, false, false,": "mlp_fwd",
     "dx_kernel<nerf::mlp::PBF3>": "mlp_bwd_dx",
+    "dx_kernel<nerf::mlp::PF32W>": "mlp_bwd_dx",  # (the wide dX, round 6)
+    "dx_kernel<nerf::mlp::PBF3W>": "mlp_bwd_dx",
+    "dx_kernel<nerf::mlp::PBF16W>": "mlp_bwd_dx",
     "dw_kernel<nerf::mlp::PBF3>": "mlp_bwd_dw",
     "fwd_kernel<nerf::mlp::PBF3W, true, false,": "mlp_fwd_train",  # (the wide bf16x3 forward, round 6)
     "fwd_kernel<nerf::mlp::PBF3W, false, false,": "mlp_fwd",
