@@ -92,6 +92,19 @@ def test_bf16x3f_dtype_maps_to_its_parts(lib):
         assert lib.nerf_mlp_dz_bytes(3, M) == lib.nerf_mlp_dz_bytes(1, M)
 
 
+def test_packed_layout_sizes(lib):
+    """The packed weight layouts (mlp_tables.h): forward 32-row units (fp32 4 KiB / bf16 2 KiB per input tile + a
+    bias chunk per unit; 592 tiles, 78 units), the wide bf16x3 forward's 16-row units (2 KiB per K-block + a bias
+    chunk; 1,172 K-blocks, 154 units), the 32x32 dX's W^T units (556 tiles) and the wide dX's 16-row W^T units (1,112
+    K-blocks, 2 KiB each: the same bytes as fp32's 32-row pack) -- fp32 and bf16x3 run the wide dX, bf16 the 32x32 one."""
+    K = 1024
+    assert lib.nerf_mlp_packed_bytes(0, 0) == (592 * 4 + 78) * K  # (PF32: the training forward too, NERF_F32_WIDE=0)
+    assert lib.nerf_mlp_packed_bytes(1, 0) == (592 * 2 + 78) * K
+    assert lib.nerf_mlp_packed_bytes(2, 0) == (1172 * 2 + 154) * K
+    assert lib.nerf_mlp_packed_bytes(0, 1) == lib.nerf_mlp_packed_bytes(2, 1) == 1112 * 2 * K == 556 * 4 * K
+    assert lib.nerf_mlp_packed_bytes(1, 1) == 556 * 2 * K
+
+
 def test_bf16x6_is_an_inference_forward_only(lib):
     """NERF_DTYPE_BF16X6 (4): a forward pack and an inference forward; no backward pack, no training
     stores, no backward, no device-count forward."""
